@@ -1,0 +1,784 @@
+// C ABI of libctg.so (include/ctg.h): host orchestration of the face scan,
+// the record sort/reduction and the result handles.
+#include <hip/hip_runtime.h>
+#include <cstring>
+#include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/device/device_run_length_encode.hpp>
+#include <rocprim/device/device_scan.hpp>
+#include <rocprim/device/device_select.hpp>
+
+#include <algorithm>
+#include <cstdio>
+#include <map>
+#include <mutex>
+
+#include "ctg_internal.h"
+
+namespace ctg {
+hipError_t launch_face_scan(const ScanParams& P, const RecordBuf& R, Counters* C, hipStream_t s);
+hipError_t launch_unique_tiles(const uint64_t* L, const int64_t* shape, const int64_t* b, const int64_t* e,
+                               uint64_t* out, unsigned long long* count, int64_t cap, hipStream_t s);
+hipError_t launch_pack_keys(int64_t n, const uint64_t* key, int nb, uint64_t* sk, uint32_t* idx, hipStream_t s);
+hipError_t launch_pack_pairs(int64_t n, const uint64_t* uv, int nb, uint64_t* sk, uint32_t* idx, hipStream_t s);
+hipError_t launch_max_pairs(int64_t n, const uint64_t* uv, unsigned long long* out, hipStream_t s);
+hipError_t launch_reduce(int64_t E, const uint64_t* uniq, const uint32_t* runs, const uint32_t* offs,
+                         const uint32_t* perm, const RecordBuf& R, int wide, int stats, int nb, int need_adj,
+                         int ignore_label, double scale, double offset, const ReduceOut& O, hipStream_t s);
+hipError_t launch_compact(int64_t E, const uint32_t* keep, const uint32_t* pos, const ReduceOut& in,
+                          const ReduceOut& out, hipStream_t s);
+hipError_t launch_endpoints(int64_t E, const uint64_t* uniq, int nb, uint32_t* out, hipStream_t s);
+hipError_t launch_u32_to_u64(int64_t n, const uint32_t* in, uint64_t* out, hipStream_t s);
+hipError_t launch_find_edges(const uint64_t* ge, int64_t n, const uint64_t* q, int64_t m, int64_t* out,
+                             hipStream_t s);
+hipError_t launch_synth(uint64_t* labels, float* boundary, const int64_t* shape, int64_t z_offset,
+                        const int64_t* gshape, int cell, uint64_t seed, uint64_t label_offset, double noise_amp,
+                        hipStream_t s);
+hipError_t launch_synth_aff(const float* b, float* out, const int64_t* shape, int n_channels, const int32_t* off,
+                            hipStream_t s);
+
+static thread_local std::string g_err;
+void set_error(const std::string& msg) { g_err = msg; }
+
+// ---------------------------------------------------------------------------
+// caching device allocator: results and scratch are recycled between calls so
+// steady-state calls do no hipMalloc/hipFree
+// ---------------------------------------------------------------------------
+static std::mutex g_mu;
+static std::multimap<size_t, void*> g_pool[64];
+
+static int cur_dev() {
+    int d = 0;
+    hipGetDevice(&d);
+    return d;
+}
+
+static size_t round_up(size_t b) {
+    size_t r = 256;
+    while (r < b) r = r < (1u << 20) ? r * 2 : r + (r >> 2);
+    return r;
+}
+
+static void* dmalloc(size_t bytes) {
+    if (bytes == 0) bytes = 256;
+    bytes = round_up(bytes);
+    const int d = cur_dev();
+    {
+        std::lock_guard<std::mutex> g(g_mu);
+        auto& pool = g_pool[d & 63];
+        auto it = pool.lower_bound(bytes);
+        if (it != pool.end() && it->first <= bytes * 2) {
+            void* p = it->second;
+            pool.erase(it);
+            return p;
+        }
+    }
+    void* p = nullptr;
+    if (hipMalloc(&p, bytes + 64) != hipSuccess) {
+        // release cached blocks and retry once
+        std::lock_guard<std::mutex> g(g_mu);
+        for (auto& kv : g_pool[d & 63]) hipFree(kv.second);
+        g_pool[d & 63].clear();
+        if (hipMalloc(&p, bytes + 64) != hipSuccess) return nullptr;
+    }
+    return p;
+}
+
+static std::map<void*, size_t> g_sizes;
+static void* dalloc(size_t bytes) {
+    bytes = round_up(bytes == 0 ? 256 : bytes);
+    void* p = dmalloc(bytes);
+    if (p) {
+        std::lock_guard<std::mutex> g(g_mu);
+        g_sizes[p] = bytes;
+    }
+    return p;
+}
+static void dfree(void* p) {
+    if (!p) return;
+    const int d = cur_dev();
+    std::lock_guard<std::mutex> g(g_mu);
+    auto it = g_sizes.find(p);
+    size_t b = it == g_sizes.end() ? 256 : it->second;
+    g_pool[d & 63].emplace(b, p);
+}
+
+void ensure(void** p, size_t& have, size_t need) {
+    if (need <= have && *p) return;
+    if (*p) dfree(*p);
+    size_t n = std::max(need, have + have / 2);
+    *p = dalloc(n);
+    have = *p ? n : 0;
+}
+
+static Workspace g_ws[64];
+Workspace& ws(int device) { return g_ws[device & 63]; }
+int current_device() { return cur_dev(); }
+
+static hipError_t ws_init(Workspace& w) {
+    if (w.counters) return hipSuccess;
+    hipError_t e = hipMalloc(&w.counters, sizeof(Counters));
+    if (e != hipSuccess) return e;
+    e = hipHostMalloc(&w.counters_host, sizeof(Counters), hipHostMallocDefault);
+    if (e != hipSuccess) return e;
+    e = hipMalloc(&w.small, 64 * sizeof(unsigned int));
+    if (e != hipSuccess) return e;
+    e = hipHostMalloc(&w.small_host, 64 * sizeof(unsigned int), hipHostMallocDefault);
+    if (e != hipSuccess) return e;
+    for (int i = 0; i < 8; ++i) hipEventCreate(&w.ev[i]);
+    w.events = true;
+    return hipSuccess;
+}
+
+hipError_t ensure_records(Workspace& w, int64_t need, int wide) {
+    if (need <= w.rec.cap && w.rec.key) return hipSuccess;
+    dfree(w.rec.key);
+    dfree(w.rec.sums);
+    dfree(w.rec.hist);
+    const int words = wide ? WREC_WORDS : NREC_WORDS;
+    w.rec.key = (uint64_t*)dalloc((size_t)need * 8);
+    w.rec.sums = (double2*)dalloc((size_t)need * 16);
+    w.rec.hist = (uint32_t*)dalloc((size_t)need * words * 4);
+    if (!w.rec.key || !w.rec.sums || !w.rec.hist) return hipErrorOutOfMemory;
+    w.rec.cap = need;
+    return hipSuccess;
+}
+
+static int bits_for(uint64_t v) {
+    int b = 1;
+    while (b < 64 && (v >> b)) ++b;
+    return b;
+}
+
+struct Ev {
+    Workspace& w;
+    hipStream_t s;
+    void mark(int i) {
+        if (w.profiling) hipEventRecord(w.ev[i], s);
+    }
+};
+
+// rocPRIM call with the shared temp buffer: size query (t == nullptr), grow, run.
+// CALL must use the names ``t`` (void*) and ``tbytes`` (size_t&).
+#define ROCPRIM_CALL(w, CALL)                                     \
+    do {                                                          \
+        void* t = nullptr;                                        \
+        size_t tbytes = 0;                                        \
+        hipError_t e_ = (CALL);                                   \
+        if (e_ != hipSuccess) return e_;                          \
+        ensure(&(w).temp, (w).temp_bytes, tbytes + 256);          \
+        if (!(w).temp) return hipErrorOutOfMemory;                \
+        t = (w).temp;                                             \
+        tbytes = (w).temp_bytes;                                  \
+        e_ = (CALL);                                              \
+        if (e_ != hipSuccess) return e_;                          \
+    } while (0)
+
+// ---------------------------------------------------------------------------
+// shared back half: records (n, with keys (u<<32|v) or (u,v) pairs) -> result
+// ---------------------------------------------------------------------------
+struct ReduceJob {
+    int64_t n;                 // records
+    const uint64_t* keys;      // packed (u<<32)|v, or null if pairs given
+    const uint64_t* pairs;     // (u,v) pairs
+    RecordBuf R;
+    int wide, stats, need_adj, ignore_label, keep_stats;
+    uint64_t max_v;
+    double scale, offset;
+    int64_t single_label_nodes;  // >=0: no edges -> nodes = this label; -1: none
+    const uint64_t* single_label_ptr;  // device pointer to a label to use if E == 0
+};
+
+static hipError_t reduce_records(Workspace& w, const ReduceJob& J, hipStream_t s, ctg_result* res) {
+    Ev ev{w, s};
+    const int64_t n = J.n;
+    const int nb = bits_for(J.max_v);
+    if (nb > 32) return hipErrorInvalidValue;
+    // sort buffers
+    if (n > w.sort_cap) {
+        dfree(w.sk_in); dfree(w.sk_out); dfree(w.idx_in); dfree(w.idx_out);
+        const int64_t cap = std::max<int64_t>(n, w.sort_cap + w.sort_cap / 2);
+        w.sk_in = (uint64_t*)dalloc(cap * 8); w.sk_out = (uint64_t*)dalloc(cap * 8);
+        w.idx_in = (uint32_t*)dalloc(cap * 4); w.idx_out = (uint32_t*)dalloc(cap * 4);
+        w.uniq = (uint64_t*)dalloc(cap * 8); w.runs = (uint32_t*)dalloc(cap * 4);
+        w.offs = (uint32_t*)dalloc(cap * 4); w.keep = (uint32_t*)dalloc(cap * 4);
+        w.pos = (uint32_t*)dalloc(cap * 4);
+        if (!w.sk_in || !w.sk_out || !w.idx_in || !w.idx_out || !w.uniq || !w.runs || !w.offs || !w.keep || !w.pos)
+            return hipErrorOutOfMemory;
+        w.sort_cap = cap;
+    }
+    hipError_t e;
+    if (J.keys) e = launch_pack_keys(n, J.keys, nb, w.sk_in, w.idx_in, s);
+    else e = launch_pack_pairs(n, J.pairs, nb, w.sk_in, w.idx_in, s);
+    if (e != hipSuccess) return e;
+    ev.mark(2);
+    ROCPRIM_CALL(w, rocprim::radix_sort_pairs(t, tbytes, w.sk_in, w.sk_out, w.idx_in, w.idx_out, (size_t)n, 0u,
+                                              (unsigned)(2 * nb), s));
+    ev.mark(3);
+    ROCPRIM_CALL(w, rocprim::run_length_encode(t, tbytes, w.sk_out, (unsigned)n, w.uniq, w.runs, w.small, s));
+    e = hipMemcpyAsync(w.small_host, w.small, sizeof(unsigned), hipMemcpyDeviceToHost, s);
+    if (e != hipSuccess) return e;
+    e = hipStreamSynchronize(s);
+    if (e != hipSuccess) return e;
+    const int64_t E_all = n ? (int64_t)w.small_host[0] : 0;
+    ROCPRIM_CALL(w, rocprim::exclusive_scan(t, tbytes, w.runs, w.offs, 0u, (size_t)E_all, rocprim::plus<uint32_t>(), s));
+    ev.mark(4);
+
+    // outputs (uncompacted)
+    const bool may_drop = J.need_adj || J.ignore_label;
+    ReduceOut O{};
+    O.edges = (uint64_t*)dalloc(std::max<int64_t>(E_all, 1) * 16);
+    O.feats = J.stats ? (double*)dalloc(std::max<int64_t>(E_all, 1) * N_FEATURES * 8) : nullptr;
+    O.keep = may_drop ? w.keep : nullptr;
+    if (J.keep_stats && J.stats) {
+        O.wstats = (uint32_t*)dalloc(std::max<int64_t>(E_all, 1) * WREC_WORDS * 4);
+        O.wsums = (double2*)dalloc(std::max<int64_t>(E_all, 1) * 16);
+    }
+    e = launch_reduce(E_all, w.uniq, w.runs, w.offs, w.idx_out, J.R, J.wide, J.stats, nb, J.need_adj,
+                      J.ignore_label, J.scale, J.offset, O, s);
+    if (e != hipSuccess) return e;
+    int64_t E = E_all;
+    if (may_drop && E_all) {
+        ROCPRIM_CALL(w, rocprim::exclusive_scan(t, tbytes, w.keep, w.pos, 0u, (size_t)E_all, rocprim::plus<uint32_t>(), s));
+        unsigned tail[2];
+        e = hipMemcpyAsync(w.small_host, w.pos + (E_all - 1), 4, hipMemcpyDeviceToHost, s);
+        if (e != hipSuccess) return e;
+        e = hipMemcpyAsync(w.small_host + 1, w.keep + (E_all - 1), 4, hipMemcpyDeviceToHost, s);
+        if (e != hipSuccess) return e;
+        e = hipStreamSynchronize(s);
+        if (e != hipSuccess) return e;
+        tail[0] = w.small_host[0];
+        tail[1] = w.small_host[1];
+        E = (int64_t)tail[0] + tail[1];
+        if (E != E_all) {
+            ReduceOut C2{};
+            C2.edges = (uint64_t*)dalloc(std::max<int64_t>(E, 1) * 16);
+            C2.feats = O.feats ? (double*)dalloc(std::max<int64_t>(E, 1) * N_FEATURES * 8) : nullptr;
+            if (O.wstats) {
+                C2.wstats = (uint32_t*)dalloc(std::max<int64_t>(E, 1) * WREC_WORDS * 4);
+                C2.wsums = (double2*)dalloc(std::max<int64_t>(E, 1) * 16);
+            }
+            e = launch_compact(E_all, w.keep, w.pos, O, C2, s);
+            if (e != hipSuccess) return e;
+            e = hipStreamSynchronize(s);
+            if (e != hipSuccess) return e;
+            dfree(O.edges); dfree(O.feats); dfree(O.wstats); dfree(O.wsums);
+            O = C2;
+        }
+    }
+    ev.mark(5);
+    res->n_edges = E;
+    res->edges = O.edges;
+    res->features = O.feats;
+    res->stats = O.wstats;
+    res->stat_sums = O.wsums;
+
+    // nodes = unique endpoints of every unique key (before filtering)
+    if (E_all > 0) {
+        uint32_t* ep = (uint32_t*)dalloc(E_all * 8);
+        uint32_t* ep2 = (uint32_t*)dalloc(E_all * 8);
+        uint32_t* nodes32 = (uint32_t*)dalloc(E_all * 8);
+        if (!ep || !ep2 || !nodes32) return hipErrorOutOfMemory;
+        e = launch_endpoints(E_all, w.uniq, nb, ep, s);
+        if (e != hipSuccess) return e;
+        ROCPRIM_CALL(w, rocprim::radix_sort_keys(t, tbytes, ep, ep2, (size_t)(2 * E_all), 0u, (unsigned)nb, s));
+        ROCPRIM_CALL(w, rocprim::unique(t, tbytes, ep2, nodes32, w.small + 1, (size_t)(2 * E_all),
+                                        rocprim::equal_to<uint32_t>(), s));
+        e = hipMemcpyAsync(w.small_host + 1, w.small + 1, 4, hipMemcpyDeviceToHost, s);
+        if (e != hipSuccess) return e;
+        e = hipStreamSynchronize(s);
+        if (e != hipSuccess) return e;
+        const int64_t N = w.small_host[1];
+        res->nodes = (uint64_t*)dalloc(std::max<int64_t>(N, 1) * 8);
+        e = launch_u32_to_u64(N, nodes32, res->nodes, s);
+        if (e != hipSuccess) return e;
+        res->n_nodes = N;
+        dfree(ep); dfree(ep2); dfree(nodes32);
+    } else if (J.single_label_ptr) {
+        res->nodes = (uint64_t*)dalloc(8);
+        e = hipMemcpyAsync(res->nodes, J.single_label_ptr, 8, hipMemcpyDeviceToDevice, s);
+        if (e != hipSuccess) return e;
+        res->n_nodes = 1;
+    } else {
+        res->nodes = (uint64_t*)dalloc(8);
+        res->n_nodes = 0;
+    }
+    ev.mark(6);
+    return hipSuccess;
+}
+
+}  // namespace ctg
+
+using namespace ctg;
+
+// ---------------------------------------------------------------------------
+// C ABI
+// ---------------------------------------------------------------------------
+extern "C" {
+
+int ctg_version(void) { return 1; }
+
+const char* ctg_last_error(void) { return g_err.c_str(); }
+
+int ctg_device_count(int* count) {
+    CTG_CHECK(hipGetDeviceCount(count));
+    return CTG_OK;
+}
+
+int ctg_init(int device) {
+    int n = 0;
+    CTG_CHECK(hipGetDeviceCount(&n));
+    if (device < 0 || device >= n) {
+        set_error("ctg_init: invalid device " + std::to_string(device));
+        return CTG_ERR_ARG;
+    }
+    CTG_CHECK(hipSetDevice(device));
+    CTG_CHECK(ws_init(ws(device)));
+    return CTG_OK;
+}
+
+int ctg_set_profiling(int on) {
+    ws(cur_dev()).profiling = on;
+    return CTG_OK;
+}
+
+int ctg_last_timings(double* ms, int n) {
+    Workspace& w = ws(cur_dev());
+    for (int i = 0; i < n && i < 8; ++i) ms[i] = w.last_ms[i];
+    return CTG_OK;
+}
+
+static int stage_in(Workspace& w, int slot, const void* src, size_t bytes, int mem, hipStream_t s,
+                    const void** dev) {
+    if (mem == CTG_MEM_DEVICE || src == nullptr) {
+        *dev = src;
+        return CTG_OK;
+    }
+    ensure(&w.stage[slot], w.stage_bytes[slot], bytes);
+    if (!w.stage[slot]) {
+        set_error("out of device memory staging input");
+        return CTG_ERR_NOMEM;
+    }
+    CTG_CHECK(hipMemcpyAsync(w.stage[slot], src, bytes, hipMemcpyHostToDevice, s));
+    *dev = w.stage[slot];
+    return CTG_OK;
+}
+
+int ctg_rag_features(const void* labels, int label_bits, const void* data, int data_kind, int n_channels,
+                     const int32_t* offsets, const int64_t* shape, const int64_t* own_begin, int ignore_label,
+                     double hist_lo, double hist_hi, int keep_stats, int mem, void* stream, ctg_result** out) {
+    if (!out || !shape || !labels) {
+        set_error("ctg_rag_features: null argument");
+        return CTG_ERR_ARG;
+    }
+    *out = nullptr;
+    if (label_bits != 32 && label_bits != 64) {
+        set_error("ctg_rag_features: label_bits must be 32 or 64");
+        return CTG_ERR_ARG;
+    }
+    if (n_channels < 0 || n_channels > CTG_MAX_CHANNELS || (n_channels > 0 && !offsets)) {
+        set_error("ctg_rag_features: bad channel/offset arguments");
+        return CTG_ERR_ARG;
+    }
+    if (data && data_kind != CTG_DATA_F32 && data_kind != CTG_DATA_U8) {
+        set_error("ctg_rag_features: data_kind must be CTG_DATA_F32 or CTG_DATA_U8");
+        return CTG_ERR_ARG;
+    }
+    if (!(hist_hi > hist_lo)) {
+        set_error("ctg_rag_features: hist_hi must be > hist_lo");
+        return CTG_ERR_ARG;
+    }
+    for (int k = 0; k < 3; ++k)
+        if (shape[k] < 0 || (own_begin && (own_begin[k] < 0))) {
+            set_error("ctg_rag_features: negative shape/own_begin");
+            return CTG_ERR_ARG;
+        }
+    const int dev = cur_dev();
+    Workspace& w = ws(dev);
+    CTG_CHECK(ws_init(w));
+    hipStream_t s = (hipStream_t)stream;
+    const int64_t V = shape[0] * shape[1] * shape[2];
+    const size_t lbytes = (size_t)V * (label_bits / 8);
+    const size_t dbytes = data ? (size_t)V * (n_channels > 0 ? n_channels : 1) * (data_kind == CTG_DATA_U8 ? 1 : 4) : 0;
+    const void* dl = nullptr;
+    const void* dd = nullptr;
+    int rc = stage_in(w, 0, labels, lbytes, mem, s, &dl);
+    if (rc) return rc;
+    rc = stage_in(w, 1, data, dbytes, mem, s, &dd);
+    if (rc) return rc;
+
+    ScanParams P;
+    std::memset(&P, 0, sizeof(P));
+    P.labels = dl;
+    P.data = dd;
+    P.label_bits = label_bits;
+    P.data_kind = data ? data_kind : CTG_DATA_NONE;
+    P.n_channels = data ? n_channels : 0;
+    for (int c = 0; c < P.n_channels; ++c)
+        for (int k = 0; k < 3; ++k) P.offsets[c][k] = offsets[3 * c + k];
+    for (int k = 0; k < 3; ++k) {
+        P.shape[k] = shape[k];
+        P.own_begin[k] = own_begin ? own_begin[k] : 0;
+    }
+    P.scale = (double)NBINS / (hist_hi - hist_lo);
+    P.offset = hist_lo;
+    // u16 histogram slots in the LDS table must not overflow within one tile:
+    // samples per entry per tile <= samples_per_voxel * 64 * 8 * tile_z < 65536
+    const int spv = P.n_channels > 0 ? std::max(P.n_channels, 3) : 6;
+    int tz = 65535 / (TILE_X * TILE_Y * spv);
+    tz = std::max(1, std::min(16, tz));
+    P.tile_z = tz;
+
+    Ev ev{w, s};
+    ev.mark(0);
+    if (V == 0) {
+        ctg_result* r = new ctg_result();
+        r->device = dev;
+        r->edges = (uint64_t*)dalloc(16);
+        r->nodes = (uint64_t*)dalloc(8);
+        *out = r;
+        return CTG_OK;
+    }
+    // record capacity: grows (and the scan re-runs) when exceeded
+    int64_t need = std::max<int64_t>(w.rec.cap, std::max<int64_t>(1 << 16, V / 24));
+    const bool stats = P.data_kind != CTG_DATA_NONE;
+    for (int attempt = 0; attempt < 4; ++attempt) {
+        CTG_CHECK(ensure_records(w, need, 0));
+        CTG_CHECK(hipMemsetAsync(w.counters, 0, sizeof(Counters), s));
+        CTG_CHECK(launch_face_scan(P, w.rec, w.counters, s));
+        ev.mark(1);
+        CTG_CHECK(hipMemcpyAsync(w.counters_host, w.counters, sizeof(Counters), hipMemcpyDeviceToHost, s));
+        CTG_CHECK(hipStreamSynchronize(s));
+        if (w.counters_host->label_overflow) {
+            set_error("ctg_rag_features: labels >= 2^32 need label_bits=32 after dense relabelling "
+                      "(use ctg_unique_labels + remap)");
+            return CTG_ERR_UNSUPPORTED;
+        }
+        if ((int64_t)w.counters_host->n_records <= w.rec.cap) break;
+        need = (int64_t)(w.counters_host->n_records * 5 / 4) + 1024;
+        if (attempt == 3) {
+            set_error("ctg_rag_features: record buffer overflow");
+            return CTG_ERR_NOMEM;
+        }
+    }
+    const int64_t n = (int64_t)w.counters_host->n_records;
+    w.last_records = n;
+    w.last_direct = (int64_t)w.counters_host->n_direct;
+
+    ctg_result* r = new ctg_result();
+    r->device = dev;
+    r->n_records = n;
+    r->n_direct = w.last_direct;
+    ReduceJob J{};
+    J.n = n;
+    J.keys = w.rec.key;
+    J.R = w.rec;
+    J.wide = 0;
+    J.stats = stats;
+    J.need_adj = P.n_channels > 0 ? 1 : 0;
+    J.ignore_label = ignore_label;
+    J.keep_stats = keep_stats;
+    J.max_v = w.counters_host->max_v;
+    J.scale = P.scale;
+    J.offset = P.offset;
+    // single-label array: the owned origin voxel is the only node
+    const int64_t o0 = own_begin ? own_begin[0] : 0, o1 = own_begin ? own_begin[1] : 0,
+                  o2 = own_begin ? own_begin[2] : 0;
+    const bool has_owned = o0 < shape[0] && o1 < shape[1] && o2 < shape[2];
+    J.single_label_ptr = (label_bits == 64 && has_owned)
+                             ? (const uint64_t*)dl + ((o0 * shape[1] + o1) * shape[2] + o2)
+                             : nullptr;
+    hipError_t e = reduce_records(w, J, s, r);
+    if (e == hipSuccess && label_bits == 32 && r->n_edges == 0 && has_owned) {
+        // 32-bit labels: widen the single label
+        uint32_t l32 = 0;
+        e = hipMemcpyAsync(&l32, (const uint32_t*)dl + ((o0 * shape[1] + o1) * shape[2] + o2), 4,
+                           hipMemcpyDeviceToHost, s);
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        uint64_t l64 = l32;
+        if (e == hipSuccess) e = hipMemcpy(r->nodes, &l64, 8, hipMemcpyHostToDevice);
+        r->n_nodes = 1;
+    }
+    if (e != hipSuccess) {
+        set_error(std::string("ctg_rag_features: ") + hipGetErrorString(e));
+        ctg_free(r);
+        return CTG_ERR_HIP;
+    }
+    if (w.profiling) {
+        CTG_CHECK(hipStreamSynchronize(s));
+        float ms = 0.f;
+        const int a[6] = {0, 1, 2, 3, 4, 5};
+        for (int i = 0; i < 6; ++i) {
+            hipEventElapsedTime(&ms, w.ev[a[i]], w.ev[a[i] + 1]);
+            w.last_ms[i] = ms;
+        }
+        hipEventElapsedTime(&ms, w.ev[0], w.ev[6]);
+        w.last_ms[6] = ms;
+    }
+    *out = r;
+    return CTG_OK;
+}
+
+int ctg_unique_labels(const uint64_t* labels, const int64_t* shape, const int64_t* begin, const int64_t* end,
+                      int mem, void* stream, ctg_result** out) {
+    if (!labels || !shape || !out) {
+        set_error("ctg_unique_labels: null argument");
+        return CTG_ERR_ARG;
+    }
+    *out = nullptr;
+    int64_t b[3], e[3];
+    for (int k = 0; k < 3; ++k) {
+        b[k] = begin ? begin[k] : 0;
+        e[k] = end ? end[k] : shape[k];
+        if (b[k] < 0 || e[k] > shape[k] || b[k] > e[k]) {
+            set_error("ctg_unique_labels: box outside the array");
+            return CTG_ERR_ARG;
+        }
+    }
+    const int dev = cur_dev();
+    Workspace& w = ws(dev);
+    CTG_CHECK(ws_init(w));
+    hipStream_t s = (hipStream_t)stream;
+    const int64_t V = shape[0] * shape[1] * shape[2];
+    const void* dl = nullptr;
+    int rc = stage_in(w, 0, labels, (size_t)V * 8, mem, s, &dl);
+    if (rc) return rc;
+    ctg_result* r = new ctg_result();
+    r->device = dev;
+    const int64_t nb = (e[0] - b[0]) * (e[1] - b[1]) * (e[2] - b[2]);
+    if (nb == 0) {
+        r->nodes = (uint64_t*)dalloc(8);
+        r->edges = (uint64_t*)dalloc(16);
+        *out = r;
+        return CTG_OK;
+    }
+    int64_t cap = std::min<int64_t>(nb, std::max<int64_t>(1 << 16, nb / 8));
+    for (int attempt = 0; attempt < 3; ++attempt) {
+        uint64_t* cand = (uint64_t*)dalloc(cap * 8);
+        uint64_t* sorted = (uint64_t*)dalloc(cap * 8);
+        r->nodes = (uint64_t*)dalloc(cap * 8);
+        CTG_CHECK(hipMemsetAsync(w.counters, 0, sizeof(Counters), s));
+        CTG_CHECK(launch_unique_tiles((const uint64_t*)dl, shape, b, e, cand, &w.counters->n_records, cap, s));
+        CTG_CHECK(hipMemcpyAsync(w.counters_host, w.counters, sizeof(Counters), hipMemcpyDeviceToHost, s));
+        CTG_CHECK(hipStreamSynchronize(s));
+        const int64_t m = (int64_t)w.counters_host->n_records;
+        if (m > cap) {
+            dfree(cand); dfree(sorted); dfree(r->nodes); r->nodes = nullptr;
+            cap = std::min<int64_t>(nb, m + 1024);
+            continue;
+        }
+        size_t tb = 0;
+        CTG_CHECK(rocprim::radix_sort_keys(nullptr, tb, cand, sorted, (size_t)m, 0u, 64u, s));
+        ensure(&w.temp, w.temp_bytes, tb + 256);
+        tb = w.temp_bytes;
+        CTG_CHECK(rocprim::radix_sort_keys(w.temp, tb, cand, sorted, (size_t)m, 0u, 64u, s));
+        tb = 0;
+        CTG_CHECK(rocprim::unique(nullptr, tb, sorted, r->nodes, w.small + 2, (size_t)m,
+                                  rocprim::equal_to<uint64_t>(), s));
+        ensure(&w.temp, w.temp_bytes, tb + 256);
+        tb = w.temp_bytes;
+        CTG_CHECK(rocprim::unique(w.temp, tb, sorted, r->nodes, w.small + 2, (size_t)m,
+                                  rocprim::equal_to<uint64_t>(), s));
+        CTG_CHECK(hipMemcpyAsync(w.small_host + 2, w.small + 2, 4, hipMemcpyDeviceToHost, s));
+        CTG_CHECK(hipStreamSynchronize(s));
+        r->n_nodes = w.small_host[2];
+        dfree(cand);
+        dfree(sorted);
+        r->edges = (uint64_t*)dalloc(16);
+        *out = r;
+        return CTG_OK;
+    }
+    set_error("ctg_unique_labels: candidate buffer overflow");
+    ctg_free(r);
+    return CTG_ERR_NOMEM;
+}
+
+int ctg_merge_stats(const uint64_t* keys, const double* sums, const uint32_t* records, int64_t n, double hist_lo,
+                    double hist_hi, int keep_stats, int mem, void* stream, ctg_result** out) {
+    if (!out || n < 0 || (n > 0 && (!keys || !sums || !records))) {
+        set_error("ctg_merge_stats: bad arguments");
+        return CTG_ERR_ARG;
+    }
+    *out = nullptr;
+    const int dev = cur_dev();
+    Workspace& w = ws(dev);
+    CTG_CHECK(ws_init(w));
+    hipStream_t s = (hipStream_t)stream;
+    ctg_result* r = new ctg_result();
+    r->device = dev;
+    if (n == 0) {
+        r->edges = (uint64_t*)dalloc(16);
+        r->nodes = (uint64_t*)dalloc(8);
+        *out = r;
+        return CTG_OK;
+    }
+    // inputs to device (merge buffers are separate from the scan records)
+    uint64_t* dk = (uint64_t*)keys;
+    double2* ds = (double2*)sums;
+    uint32_t* dr = (uint32_t*)records;
+    bool owned = false;
+    if (mem == CTG_MEM_HOST) {
+        dk = (uint64_t*)dalloc(n * 16);
+        ds = (double2*)dalloc(n * 16);
+        dr = (uint32_t*)dalloc(n * WREC_WORDS * 4);
+        if (!dk || !ds || !dr) {
+            set_error("ctg_merge_stats: out of device memory");
+            return CTG_ERR_NOMEM;
+        }
+        CTG_CHECK(hipMemcpyAsync(dk, keys, n * 16, hipMemcpyHostToDevice, s));
+        CTG_CHECK(hipMemcpyAsync(ds, sums, n * 16, hipMemcpyHostToDevice, s));
+        CTG_CHECK(hipMemcpyAsync(dr, records, n * WREC_WORDS * 4, hipMemcpyHostToDevice, s));
+        owned = true;
+    }
+    CTG_CHECK(hipMemsetAsync(w.counters, 0, sizeof(Counters), s));
+    CTG_CHECK(launch_max_pairs(n, dk, &w.counters->max_v, s));
+    CTG_CHECK(hipMemcpyAsync(w.counters_host, w.counters, sizeof(Counters), hipMemcpyDeviceToHost, s));
+    CTG_CHECK(hipStreamSynchronize(s));
+    if (w.counters_host->max_v >> 32) {
+        set_error("ctg_merge_stats: labels >= 2^32 are not supported by the merge");
+        delete r;
+        return CTG_ERR_UNSUPPORTED;
+    }
+    ReduceJob J{};
+    J.n = n;
+    J.pairs = dk;
+    J.R.key = nullptr;
+    J.R.sums = ds;
+    J.R.hist = dr;
+    J.R.cap = n;
+    J.wide = 1;
+    J.stats = 1;
+    J.need_adj = 1;
+    J.ignore_label = 0;
+    J.keep_stats = keep_stats;
+    J.max_v = w.counters_host->max_v;
+    J.scale = (double)NBINS / (hist_hi - hist_lo);
+    J.offset = hist_lo;
+    hipError_t e = reduce_records(w, J, s, r);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (owned) {
+        dfree(dk);
+        dfree(ds);
+        dfree(dr);
+    }
+    if (e != hipSuccess) {
+        set_error(std::string("ctg_merge_stats: ") + hipGetErrorString(e));
+        ctg_free(r);
+        return CTG_ERR_HIP;
+    }
+    *out = r;
+    return CTG_OK;
+}
+
+int ctg_map_edge_ids(const uint64_t* global_edges, int64_t n_global, const uint64_t* query, int64_t n_query,
+                     int64_t* out_ids, int mem, void* stream) {
+    if (n_global < 0 || n_query < 0 || (n_query > 0 && (!query || !out_ids))) {
+        set_error("ctg_map_edge_ids: bad arguments");
+        return CTG_ERR_ARG;
+    }
+    if (n_query == 0) return CTG_OK;
+    hipStream_t s = (hipStream_t)stream;
+    if (mem == CTG_MEM_DEVICE) {
+        CTG_CHECK(launch_find_edges(global_edges, n_global, query, n_query, out_ids, s));
+        return CTG_OK;
+    }
+    uint64_t* g = (uint64_t*)dalloc(std::max<int64_t>(n_global, 1) * 16);
+    uint64_t* q = (uint64_t*)dalloc(n_query * 16);
+    int64_t* o = (int64_t*)dalloc(n_query * 8);
+    if (!g || !q || !o) {
+        set_error("ctg_map_edge_ids: out of device memory");
+        return CTG_ERR_NOMEM;
+    }
+    if (n_global) CTG_CHECK(hipMemcpyAsync(g, global_edges, n_global * 16, hipMemcpyHostToDevice, s));
+    CTG_CHECK(hipMemcpyAsync(q, query, n_query * 16, hipMemcpyHostToDevice, s));
+    CTG_CHECK(launch_find_edges(g, n_global, q, n_query, o, s));
+    CTG_CHECK(hipMemcpyAsync(out_ids, o, n_query * 8, hipMemcpyDeviceToHost, s));
+    CTG_CHECK(hipStreamSynchronize(s));
+    dfree(g);
+    dfree(q);
+    dfree(o);
+    return CTG_OK;
+}
+
+int64_t ctg_result_num_edges(const ctg_result* r) { return r ? r->n_edges : -1; }
+int64_t ctg_result_num_nodes(const ctg_result* r) { return r ? r->n_nodes : -1; }
+
+static int copy_out(void* dst, const void* src, size_t bytes, int mem) {
+    if (bytes == 0) return CTG_OK;
+    if (!dst || !src) {
+        set_error("copy: null pointer");
+        return CTG_ERR_ARG;
+    }
+    CTG_CHECK(hipMemcpy(dst, src, bytes, mem == CTG_MEM_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost));
+    return CTG_OK;
+}
+
+int ctg_result_copy_edges(const ctg_result* r, uint64_t* dst, int mem) {
+    return copy_out(dst, r->edges, (size_t)r->n_edges * 16, mem);
+}
+int ctg_result_copy_nodes(const ctg_result* r, uint64_t* dst, int mem) {
+    return copy_out(dst, r->nodes, (size_t)r->n_nodes * 8, mem);
+}
+int ctg_result_copy_features(const ctg_result* r, double* dst, int mem) {
+    if (!r->features && r->n_edges) {
+        set_error("result has no features (graph-only call)");
+        return CTG_ERR_ARG;
+    }
+    return copy_out(dst, r->features, (size_t)r->n_edges * N_FEATURES * 8, mem);
+}
+int ctg_result_copy_stats(const ctg_result* r, double* sums_dst, uint32_t* records_dst, int mem) {
+    if (!r->stats && r->n_edges) {
+        set_error("result has no statistics (call with keep_stats=1 and data)");
+        return CTG_ERR_ARG;
+    }
+    int rc = copy_out(sums_dst, r->stat_sums, (size_t)r->n_edges * 16, mem);
+    if (rc) return rc;
+    return copy_out(records_dst, r->stats, (size_t)r->n_edges * WREC_WORDS * 4, mem);
+}
+const uint64_t* ctg_result_device_edges(const ctg_result* r) { return r ? r->edges : nullptr; }
+const double* ctg_result_device_features(const ctg_result* r) { return r ? r->features : nullptr; }
+int ctg_result_info(const ctg_result* r, int64_t* n_records, int64_t* n_direct) {
+    if (!r) return CTG_ERR_ARG;
+    if (n_records) *n_records = r->n_records;
+    if (n_direct) *n_direct = r->n_direct;
+    return CTG_OK;
+}
+
+void ctg_free(ctg_result* r) {
+    if (!r) return;
+    int d = cur_dev();
+    if (r->device >= 0 && r->device != d) hipSetDevice(r->device);
+    dfree(r->edges);
+    dfree(r->nodes);
+    dfree(r->features);
+    dfree(r->stats);
+    dfree(r->stat_sums);
+    if (r->device >= 0 && r->device != d) hipSetDevice(d);
+    delete r;
+}
+
+int ctg_synth_volume(uint64_t* labels, float* boundary, const int64_t* shape, int64_t z_offset,
+                     const int64_t* global_shape, int cell, uint64_t seed, uint64_t label_offset, double noise_amp,
+                     void* stream) {
+    if (!labels || !shape || cell <= 0) {
+        set_error("ctg_synth_volume: bad arguments");
+        return CTG_ERR_ARG;
+    }
+    int64_t g[3] = {z_offset + shape[0], shape[1], shape[2]};
+    if (global_shape)
+        for (int k = 0; k < 3; ++k) g[k] = global_shape[k];
+    CTG_CHECK(launch_synth(labels, boundary, shape, z_offset, g, cell, seed, label_offset, noise_amp,
+                           (hipStream_t)stream));
+    return CTG_OK;
+}
+
+int ctg_synth_affinities(const float* boundary, float* affs, const int64_t* shape, int n_channels,
+                         const int32_t* offsets, void* stream) {
+    if (!boundary || !affs || !shape || !offsets || n_channels <= 0) {
+        set_error("ctg_synth_affinities: bad arguments");
+        return CTG_ERR_ARG;
+    }
+    CTG_CHECK(launch_synth_aff(boundary, affs, shape, n_channels, offsets, (hipStream_t)stream));
+    return CTG_OK;
+}
+
+}  // extern "C"

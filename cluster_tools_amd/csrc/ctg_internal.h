@@ -1,0 +1,157 @@
+// Internal definitions shared by the ctg (cluster-tools graph) HIP sources.
+// gfx950 / CDNA4 only.  See DESIGN.md for the data layout and the pipeline.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include <cstddef>
+#include <string>
+#include <vector>
+
+#include "../../include/ctg.h"
+
+namespace ctg {
+
+// ---------------------------------------------------------------------------
+// fixed geometry of the face-scan tiles and the LDS edge table
+// ---------------------------------------------------------------------------
+constexpr int WAVE = 64;
+constexpr int SCAN_THREADS = 256;      // 4 waves per workgroup
+constexpr int TILE_X = 64;             // one wave row
+constexpr int TILE_Y = 8;
+constexpr int TABLE_CAP = 512;         // LDS edge-table entries (power of two)
+constexpr int NBINS = 40;              // vigra UserRangeHistogram<40> (nifty default)
+constexpr int NSLOTS = NBINS + 2;      // left outliers, 40 bins, right outliers
+constexpr int HWORDS = 21;             // 42 u16 slots packed in 21 u32 words
+constexpr int NREC_WORDS = 24;         // narrow record: 21 hist words + cnt + min + max
+constexpr int WREC_WORDS = 48;         // wide record: 42 u32 slots + cnt + min + max + pad
+constexpr uint32_t ADJ_FLAG = 0x80000000u;  // record/edge came from a nearest-neighbour face
+constexpr uint64_t EMPTY_KEY = ~0ull;
+constexpr int N_FEATURES = 10;
+
+// order-preserving float <-> u32 mapping for LDS/global atomicMin/Max
+__host__ __device__ inline uint32_t f2ord(float f) {
+    uint32_t b;
+    __builtin_memcpy(&b, &f, 4);
+    return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+}
+__host__ __device__ inline float ord2f(uint32_t o) {
+    uint32_t b = (o & 0x80000000u) ? (o & 0x7FFFFFFFu) : ~o;
+    float f;
+    __builtin_memcpy(&f, &b, 4);
+    return f;
+}
+constexpr uint32_t ORD_POS_INF = 0xFF800000u;  // f2ord(+inf)
+constexpr uint32_t ORD_NEG_INF = 0x007FFFFFu;  // f2ord(-inf)
+
+// vigra RangeHistogramBase::update binning -> slot in [0, NSLOTS)
+__host__ __device__ inline int hist_slot(double x, double scale, double offset) {
+    double m = scale * (x - offset);
+    if (m == (double)NBINS) return NBINS;          // index nbins-1 -> slot nbins
+    if (!(m < (double)NBINS)) return (m != m) ? 0 : NBINS + 1;  // right outlier (NaN -> left)
+    if (m <= -1.0) return 0;                          // (int)m < 0 -> left outlier
+    return (int)m + 1;                                // trunc toward zero, as (int)m
+}
+
+__host__ __device__ inline uint32_t hash_key(uint64_t k) {
+    k ^= k >> 33;
+    k *= 0xff51afd7ed558ccdull;
+    k ^= k >> 33;
+    return (uint32_t)k;
+}
+
+// ---------------------------------------------------------------------------
+// records: the face scan flushes one record per (tile, edge)
+// ---------------------------------------------------------------------------
+struct RecordBuf {
+    uint64_t* key = nullptr;      // (u << 32) | v
+    double2* sums = nullptr;      // (sum, sum of squares)
+    uint32_t* hist = nullptr;     // NREC_WORDS (narrow) or WREC_WORDS (wide) per record
+    int64_t cap = 0;
+};
+
+struct ScanParams {
+    const void* labels;
+    const void* data;          // boundary (Z,Y,X) or affinities (C,Z,Y,X); may be null
+    int label_bits;            // 64 or 32
+    int data_kind;             // CTG_DATA_*
+    int n_channels;            // 0 -> boundary map
+    int offsets[CTG_MAX_CHANNELS][3];
+    int64_t shape[3];
+    int64_t own_begin[3];
+    double scale, offset;      // histogram mapping
+    double u8_scale;           // uint8 -> float factor (1/255)
+    int tile_z;
+};
+
+struct Counters {               // device-side counters, zeroed per call
+    unsigned long long n_records;
+    unsigned long long n_direct;     // faces emitted past a full LDS table
+    unsigned long long label_overflow;  // labels >= 2^32 seen by the 32-bit key path
+    unsigned long long max_v;        // largest label in any key
+    unsigned long long pad[4];
+};
+
+struct ReduceOut {
+    uint64_t* edges;      // 2E
+    double* feats;        // 10E or null
+    uint32_t* keep;       // E or null
+    uint32_t* wstats;     // WREC_WORDS*E or null
+    double2* wsums;       // E or null
+};
+
+struct Workspace {
+    int device = -1;
+    RecordBuf rec;
+    // sort / reduce scratch
+    uint64_t* sk_in = nullptr; uint64_t* sk_out = nullptr;
+    uint32_t* idx_in = nullptr; uint32_t* idx_out = nullptr;
+    int64_t sort_cap = 0;
+    uint64_t* uniq = nullptr; uint32_t* runs = nullptr; uint32_t* offs = nullptr;
+    uint32_t* keep = nullptr; uint32_t* pos = nullptr;
+    int64_t edge_cap = 0;
+    void* temp = nullptr; size_t temp_bytes = 0;
+    Counters* counters = nullptr;        // device
+    Counters* counters_host = nullptr;   // pinned
+    unsigned int* small = nullptr;       // device scalars (run counts etc.)
+    unsigned int* small_host = nullptr;
+    // host->device staging of volumes
+    void* stage[2] = {nullptr, nullptr};
+    size_t stage_bytes[2] = {0, 0};
+    // timing
+    hipEvent_t ev[8];
+    bool events = false;
+    double last_ms[8] = {0};
+    int64_t last_records = 0, last_direct = 0;
+    int profiling = 0;
+};
+
+Workspace& ws(int device);
+int current_device();
+void set_error(const std::string& msg);
+void ensure(void** p, size_t& have, size_t need);
+hipError_t ensure_records(Workspace& w, int64_t need, int wide);
+
+}  // namespace ctg
+
+// result handle (opaque in the C ABI)
+struct ctg_result {
+    int device = -1;
+    int64_t n_edges = 0;
+    int64_t n_nodes = 0;
+    uint64_t* edges = nullptr;      // device (E,2)
+    uint64_t* nodes = nullptr;      // device (N,)
+    double* features = nullptr;     // device (E,10) or null
+    uint32_t* stats = nullptr;      // device wide records (E, WREC_WORDS) or null
+    double2* stat_sums = nullptr;   // device (E,) (sum, sumsq) or null
+    int64_t n_records = 0;
+    int64_t n_direct = 0;
+};
+
+#define CTG_CHECK(expr)                                                        \
+    do {                                                                       \
+        hipError_t e_ = (expr);                                                \
+        if (e_ != hipSuccess) {                                                \
+            ctg::set_error(std::string(#expr) + ": " + hipGetErrorString(e_)); \
+            return CTG_ERR_HIP;                                                \
+        }                                                                      \
+    } while (0)

@@ -1,0 +1,303 @@
+"""Array-level API over libctg.so: RAG + edge features of a label volume.
+
+Inputs are numpy arrays (host memory, results come back as numpy) or torch
+CUDA tensors (device memory, results stay resident as torch tensors).  This is
+the layer that ``cluster_tools_amd.ndist`` (the ``nifty.distributed`` mirror)
+calls after reading blocks from N5.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from . import _lib as L
+
+N_FEATURES = L.CTG_N_FEATURES
+NBINS = L.CTG_NBINS
+WIDE_WORDS = L.CTG_WIDE_RECORD_WORDS
+
+
+def _is_torch(x):
+    try:
+        import torch
+        return isinstance(x, torch.Tensor)
+    except Exception:  # pragma: no cover
+        return False
+
+
+def _ptr(x):
+    if x is None:
+        return None
+    if _is_torch(x):
+        return ctypes.c_void_p(x.data_ptr())
+    return x.ctypes.data_as(ctypes.c_void_p)
+
+
+def _shape_arr(vals):
+    return (ctypes.c_int64 * 3)(*[int(v) for v in vals])
+
+
+class Result:
+    """Owning wrapper around a ``ctg_result*`` handle (device-resident)."""
+
+    def __init__(self, handle, device):
+        self.handle = handle
+        self.device = device
+
+    def __del__(self):
+        self.free()
+
+    def free(self):
+        if getattr(self, 'handle', None):
+            L.load().ctg_free(self.handle)
+            self.handle = None
+
+    @property
+    def n_edges(self):
+        return int(L.load().ctg_result_num_edges(self.handle))
+
+    @property
+    def n_nodes(self):
+        return int(L.load().ctg_result_num_nodes(self.handle))
+
+    def info(self):
+        a, b = ctypes.c_int64(), ctypes.c_int64()
+        L.check(L.load().ctg_result_info(self.handle, ctypes.byref(a), ctypes.byref(b)), 'ctg_result_info')
+        return int(a.value), int(b.value)
+
+    # --- host copies
+    def edges(self):
+        out = np.empty((self.n_edges, 2), dtype=np.uint64)
+        L.check(L.load().ctg_result_copy_edges(self.handle, _ptr(out), L.CTG_MEM_HOST), 'copy_edges')
+        return out
+
+    def nodes(self):
+        out = np.empty(self.n_nodes, dtype=np.uint64)
+        L.check(L.load().ctg_result_copy_nodes(self.handle, _ptr(out), L.CTG_MEM_HOST), 'copy_nodes')
+        return out
+
+    def features(self):
+        out = np.empty((self.n_edges, N_FEATURES), dtype=np.float64)
+        L.check(L.load().ctg_result_copy_features(self.handle, _ptr(out), L.CTG_MEM_HOST), 'copy_features')
+        return out
+
+    def stats(self):
+        """(sums (E,2) float64, records (E,48) uint32) wide statistics."""
+        s = np.empty((self.n_edges, 2), dtype=np.float64)
+        r = np.empty((self.n_edges, WIDE_WORDS), dtype=np.uint32)
+        L.check(L.load().ctg_result_copy_stats(self.handle, _ptr(s), _ptr(r), L.CTG_MEM_HOST), 'copy_stats')
+        return s, r
+
+    # --- device copies (torch)
+    def _torch_copy(self, shape, dtype, fn):
+        import torch
+        t = torch.empty(shape, dtype=dtype, device='cuda:%d' % self.device)
+        L.check(fn(self.handle, ctypes.c_void_p(t.data_ptr()), L.CTG_MEM_DEVICE), 'device copy')
+        return t
+
+    def edges_torch(self):
+        import torch
+        t = self._torch_copy((self.n_edges, 2), torch.int64, L.load().ctg_result_copy_edges)
+        return t.view(torch.uint64) if hasattr(torch, 'uint64') else t
+
+    def features_torch(self):
+        import torch
+        return self._torch_copy((self.n_edges, N_FEATURES), torch.float64, L.load().ctg_result_copy_features)
+
+    def stats_torch(self):
+        import torch
+        s = torch.empty((self.n_edges, 2), dtype=torch.float64, device='cuda:%d' % self.device)
+        r = torch.empty((self.n_edges, WIDE_WORDS), dtype=torch.int32, device='cuda:%d' % self.device)
+        L.check(L.load().ctg_result_copy_stats(self.handle, ctypes.c_void_p(s.data_ptr()),
+                                               ctypes.c_void_p(r.data_ptr()), L.CTG_MEM_DEVICE), 'copy_stats')
+        return s, r
+
+
+def _current_stream(tensor_input):
+    if not tensor_input:
+        return None
+    import torch
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def _check_offsets(offsets):
+    off = np.ascontiguousarray(np.asarray(offsets, dtype=np.int32).reshape(-1, 3))
+    if off.shape[0] > L.CTG_MAX_CHANNELS:
+        raise ValueError('at most %d affinity channels are supported' % L.CTG_MAX_CHANNELS)
+    return off
+
+
+def rag_features_handle(labels, data=None, offsets=None, own_begin=None, ignore_label=False,
+                        hist_range=(0.0, 1.0), keep_stats=False, stream=None):
+    """Run the hot path and return the device-resident ``Result`` handle.
+
+    labels: (Z,Y,X) uint64/uint32 numpy array or CUDA tensor (int64/int32 views
+    of unsigned labels are accepted for torch); data: None, (Z,Y,X) boundary
+    map or (C,Z,Y,X) affinities (float32 or uint8); offsets: C x 3 for
+    affinities.
+    """
+    lib = L.load()
+    dev = L.init_device()
+    on_dev = _is_torch(labels)
+    if on_dev:
+        import torch
+        assert labels.is_cuda and labels.is_contiguous(), 'labels must be a contiguous CUDA tensor'
+        label_bits = labels.element_size() * 8
+        shape = tuple(labels.shape)
+        if data is not None:
+            assert _is_torch(data) and data.is_cuda and data.is_contiguous()
+            kind = L.CTG_DATA_U8 if data.dtype == torch.uint8 else L.CTG_DATA_F32
+            if kind == L.CTG_DATA_F32:
+                assert data.dtype == torch.float32
+    else:
+        labels = np.asarray(labels)
+        if labels.dtype not in (np.uint64, np.uint32, np.int64, np.int32):
+            labels = labels.astype(np.uint64)
+        labels = np.ascontiguousarray(labels)
+        label_bits = labels.dtype.itemsize * 8
+        shape = labels.shape
+        if data is not None:
+            data = np.asarray(data)
+            if data.dtype == np.uint8:
+                kind = L.CTG_DATA_U8
+            else:
+                kind = L.CTG_DATA_F32
+                data = data.astype(np.float32, copy=False)
+            data = np.ascontiguousarray(data)
+    if len(shape) != 3:
+        raise ValueError('labels must be 3-D, got shape %s' % (shape,))
+    n_ch = 0
+    off_ptr = None
+    off = None
+    if data is None:
+        kind = L.CTG_DATA_NONE
+    elif offsets is not None:
+        off = _check_offsets(offsets)
+        n_ch = off.shape[0]
+        if tuple(data.shape) != (n_ch,) + tuple(shape):
+            raise ValueError('affinities must be (C,Z,Y,X) = %s, got %s' % ((n_ch,) + tuple(shape),
+                                                                           tuple(data.shape)))
+        off_ptr = off.ctypes.data_as(ctypes.c_void_p)
+    else:
+        if tuple(data.shape) != tuple(shape):
+            raise ValueError('boundary map shape %s != labels shape %s' % (tuple(data.shape), tuple(shape)))
+    sh = _shape_arr(shape)
+    ob = _shape_arr(own_begin) if own_begin is not None else None
+    if stream is None:
+        stream = _current_stream(on_dev)
+    h = ctypes.c_void_p()
+    rc = lib.ctg_rag_features(_ptr(labels), label_bits, _ptr(data), kind, n_ch, off_ptr, sh, ob,
+                              int(bool(ignore_label)), float(hist_range[0]), float(hist_range[1]),
+                              int(bool(keep_stats)), L.CTG_MEM_DEVICE if on_dev else L.CTG_MEM_HOST,
+                              stream, ctypes.byref(h))
+    L.check(rc, 'ctg_rag_features')
+    return Result(h, dev)
+
+
+def rag_features(labels, data=None, offsets=None, own_begin=None, ignore_label=False,
+                 hist_range=(0.0, 1.0), keep_stats=False):
+    """Host convenience: returns dict(edges, nodes, features[, sums, records])."""
+    r = rag_features_handle(labels, data, offsets, own_begin, ignore_label, hist_range, keep_stats)
+    out = dict(edges=r.edges(), nodes=r.nodes())
+    if data is not None:
+        out['features'] = r.features()
+        if keep_stats:
+            out['sums'], out['records'] = r.stats()
+    out['n_records'], out['n_direct'] = r.info()
+    r.free()
+    return out
+
+
+def unique_labels(labels, begin=None, end=None):
+    """Sorted unique labels of labels[begin:end] (uint64 numpy array)."""
+    lib = L.load()
+    L.init_device()
+    on_dev = _is_torch(labels)
+    if not on_dev:
+        labels = np.ascontiguousarray(np.asarray(labels).astype(np.uint64, copy=False))
+    shape = tuple(labels.shape)
+    h = ctypes.c_void_p()
+    rc = lib.ctg_unique_labels(_ptr(labels), _shape_arr(shape),
+                               _shape_arr(begin) if begin is not None else None,
+                               _shape_arr(end) if end is not None else None,
+                               L.CTG_MEM_DEVICE if on_dev else L.CTG_MEM_HOST,
+                               _current_stream(on_dev), ctypes.byref(h))
+    L.check(rc, 'ctg_unique_labels')
+    r = Result(h, L.init_device())
+    nodes = r.nodes()
+    r.free()
+    return nodes
+
+
+def merge_stats(keys, sums, records, hist_range=(0.0, 1.0), keep_stats=False):
+    """Combine partial statistics tables (wide records) -> dict(edges, features[, sums, records])."""
+    lib = L.load()
+    dev = L.init_device()
+    keys = np.ascontiguousarray(np.asarray(keys, dtype=np.uint64).reshape(-1, 2))
+    sums = np.ascontiguousarray(np.asarray(sums, dtype=np.float64).reshape(-1, 2))
+    records = np.ascontiguousarray(np.asarray(records, dtype=np.uint32).reshape(-1, WIDE_WORDS))
+    n = keys.shape[0]
+    assert sums.shape[0] == n and records.shape[0] == n
+    h = ctypes.c_void_p()
+    rc = lib.ctg_merge_stats(_ptr(keys), _ptr(sums), _ptr(records), n, float(hist_range[0]),
+                             float(hist_range[1]), int(bool(keep_stats)), L.CTG_MEM_HOST, None, ctypes.byref(h))
+    L.check(rc, 'ctg_merge_stats')
+    r = Result(h, dev)
+    out = dict(edges=r.edges(), features=r.features())
+    if keep_stats:
+        out['sums'], out['records'] = r.stats()
+    r.free()
+    return out
+
+
+def map_edge_ids(global_edges, query):
+    """Row of every query (u,v) in the sorted global edge table (-1 if absent)."""
+    lib = L.load()
+    L.init_device()
+    g = np.ascontiguousarray(np.asarray(global_edges, dtype=np.uint64).reshape(-1, 2))
+    q = np.ascontiguousarray(np.asarray(query, dtype=np.uint64).reshape(-1, 2))
+    out = np.empty(q.shape[0], dtype=np.int64)
+    rc = lib.ctg_map_edge_ids(_ptr(g), g.shape[0], _ptr(q), q.shape[0], _ptr(out), L.CTG_MEM_HOST, None)
+    L.check(rc, 'ctg_map_edge_ids')
+    return out
+
+
+def synth_volume(shape, cell=10, seed=0, z_offset=0, global_shape=None, label_offset=0, noise_amp=0.1,
+                 with_boundary=True, device=None):
+    """Generate the synthetic volume directly in HBM (torch tensors)."""
+    import torch
+    lib = L.load()
+    dev = L.init_device(device)
+    labels = torch.empty(tuple(shape), dtype=torch.int64, device='cuda:%d' % dev)
+    bnd = torch.empty(tuple(shape), dtype=torch.float32, device='cuda:%d' % dev) if with_boundary else None
+    gs = _shape_arr(global_shape) if global_shape is not None else None
+    rc = lib.ctg_synth_volume(_ptr(labels), _ptr(bnd), _shape_arr(shape), int(z_offset), gs, int(cell),
+                              int(seed), int(label_offset), float(noise_amp),
+                              ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+    L.check(rc, 'ctg_synth_volume')
+    return labels, bnd
+
+
+def synth_affinities(boundary, offsets):
+    import torch
+    lib = L.load()
+    off = _check_offsets(offsets)
+    shape = tuple(boundary.shape)
+    affs = torch.empty((off.shape[0],) + shape, dtype=torch.float32, device=boundary.device)
+    rc = lib.ctg_synth_affinities(_ptr(boundary), _ptr(affs), _shape_arr(shape), off.shape[0],
+                                  off.ctypes.data_as(ctypes.c_void_p),
+                                  ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+    L.check(rc, 'ctg_synth_affinities')
+    return affs
+
+
+def set_profiling(on=True):
+    L.check(L.load().ctg_set_profiling(int(bool(on))), 'ctg_set_profiling')
+
+
+def last_timings():
+    """Device ms of the last rag call: scan, pack, sort, segment, reduce, nodes, total."""
+    buf = (ctypes.c_double * 7)()
+    L.check(L.load().ctg_last_timings(buf, 7), 'ctg_last_timings')
+    return dict(zip(['scan', 'pack', 'sort', 'segment', 'reduce', 'nodes', 'total'], list(buf)))

@@ -1,0 +1,138 @@
+/*
+ * ctg.h -- C ABI of the MI355X-native RAG + edge-feature library (libctg.so).
+ *
+ * This is the drop-in boundary for the hot path of cluster_tools' multicut
+ * feature stage.  In the reference, the job bodies call the pybind11 module
+ * ``nifty.distributed`` (C++, third party, pinned nifty >=v1.0.7 in
+ * conda-recipe/meta.yaml:30).  Each entry point below replaces the array-level
+ * work of one of those calls; the N5 I/O those calls do stays in the Python
+ * host layer (cluster_tools_amd/ndist.py), which mirrors the reference's
+ * function names and arguments:
+ *
+ *   ctg_rag_features(... data=NULL)   <- ndist.computeMergeableRegionGraph
+ *                                        graph/initial_sub_graphs.py:124-129
+ *   ctg_rag_features(... boundary)    <- ndist.extractBlockFeaturesFromBoundaryMaps_{float32,uint8}
+ *                                        features/block_edge_features.py:127-134
+ *   ctg_rag_features(... affinities)  <- ndist.extractBlockFeaturesFromAffinityMaps_{float32,uint8}
+ *                                        features/block_edge_features.py:138-145
+ *   ctg_merge_stats                   <- ndist.mergeSubgraphs / ndist.mergeFeatureBlocks
+ *                                        graph/merge_sub_graphs.py:130-135,
+ *                                        features/merge_edge_features.py:141-147
+ *   ctg_map_edge_ids                  <- ndist.mapEdgeIds / Graph.findEdges
+ *                                        graph/map_edge_ids.py:116-119, test/graph/test_graph.py:92
+ *   ctg_unique_labels                 <- the per-block ``nodes`` of computeMergeableRegionGraph
+ *                                        test/graph/test_graph.py:53-60
+ *
+ * Conventions: plain pointers and sizes; ``mem`` says whether array
+ * arguments live in host memory (CTG_MEM_HOST) or in device memory of the
+ * current HIP device (CTG_MEM_DEVICE); ``stream`` is a hipStream_t (NULL =
+ * default stream).  Every function returns CTG_OK (0) or a negative status;
+ * ctg_last_error() returns a thread-local message (the Python shim raises
+ * RuntimeError with it, as pybind11 does for nifty's C++ exceptions).
+ * Results are library-owned handles released with ctg_free().
+ */
+#ifndef CTG_H_
+#define CTG_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CTG_OK 0
+#define CTG_ERR_ARG -1
+#define CTG_ERR_HIP -2
+#define CTG_ERR_NOMEM -3
+#define CTG_ERR_UNSUPPORTED -4
+
+#define CTG_MEM_HOST 0
+#define CTG_MEM_DEVICE 1
+
+#define CTG_DATA_NONE 0   /* graph only */
+#define CTG_DATA_F32 1
+#define CTG_DATA_U8 2     /* mapped to [0,1] by /255 before binning (SURVEY OPEN-7) */
+
+#define CTG_MAX_CHANNELS 32
+#define CTG_N_FEATURES 10
+#define CTG_NBINS 40
+#define CTG_WIDE_RECORD_WORDS 48  /* u32 words of one wide statistics record */
+
+typedef struct ctg_result ctg_result;
+
+/* version / device */
+int ctg_version(void);
+int ctg_init(int device);
+const char* ctg_last_error(void);
+int ctg_device_count(int* count);
+
+/*
+ * RAG (+ edge features) of one 3-D label array.
+ *   labels     uint64 (label_bits=64) or uint32 (label_bits=32), C-order (Z,Y,X)
+ *   data       NULL, boundary map (Z,Y,X) or channel-first affinities (C,Z,Y,X)
+ *   offsets    NULL for a boundary map, else n_channels x 3 int32 (z,y,x) offsets
+ *   own_begin  faces / samples are counted only when their owning voxel lies in
+ *              [own_begin, shape): the upper voxel of a face, the voxel p of an
+ *              affinity sample.  NULL = whole array.  A 1-voxel own_begin is the
+ *              lower-halo geometry of increaseRoi=True.
+ *   ignore_label  drop edges that contain label 0 (nodes still contain 0)
+ *   hist_lo/hi    histogram range (nifty: [0,1])
+ * Result: sorted unique edges (u<v, lexicographic), sorted unique nodes and,
+ * if data != NULL, an (E,10) float64 feature table
+ * [mean, var, min, q10, q25, q50, q75, q90, max, count].
+ */
+int ctg_rag_features(const void* labels, int label_bits,
+                     const void* data, int data_kind,
+                     int n_channels, const int32_t* offsets,
+                     const int64_t* shape, const int64_t* own_begin,
+                     int ignore_label, double hist_lo, double hist_hi,
+                     int keep_stats, int mem, void* stream, ctg_result** out);
+
+/* sorted unique labels of labels[begin:end] (box in array coordinates) */
+int ctg_unique_labels(const uint64_t* labels, const int64_t* shape,
+                      const int64_t* begin, const int64_t* end,
+                      int mem, void* stream, ctg_result** out);
+
+/* Combine partial statistics tables (wide records, one per (part, edge)) into
+ * one table: counts add, sums add, min/max elementwise, histograms add.
+ *   keys     n x 2 uint64 (u,v) per record; sums n x 2 float64 (sum, sumsq);
+ *   records  n x CTG_WIDE_RECORD_WORDS uint32. */
+int ctg_merge_stats(const uint64_t* keys, const double* sums, const uint32_t* records,
+                    int64_t n, double hist_lo, double hist_hi, int keep_stats,
+                    int mem, void* stream, ctg_result** out);
+
+/* position of each query (u,v) in the sorted global edge table, -1 if absent */
+int ctg_map_edge_ids(const uint64_t* global_edges, int64_t n_global,
+                     const uint64_t* query, int64_t n_query, int64_t* out_ids,
+                     int mem, void* stream);
+
+/* result accessors; dst lives in host (CTG_MEM_HOST) or device memory */
+int64_t ctg_result_num_edges(const ctg_result* r);
+int64_t ctg_result_num_nodes(const ctg_result* r);
+int ctg_result_copy_edges(const ctg_result* r, uint64_t* dst, int mem);
+int ctg_result_copy_nodes(const ctg_result* r, uint64_t* dst, int mem);
+int ctg_result_copy_features(const ctg_result* r, double* dst, int mem);
+int ctg_result_copy_stats(const ctg_result* r, double* sums_dst, uint32_t* records_dst, int mem);
+/* device pointers for zero-copy consumers (valid until ctg_free) */
+const uint64_t* ctg_result_device_edges(const ctg_result* r);
+const double* ctg_result_device_features(const ctg_result* r);
+int ctg_result_info(const ctg_result* r, int64_t* n_records, int64_t* n_direct);
+void ctg_free(ctg_result* r);
+
+/* deterministic synthetic volumes (Voronoi supervoxels + boundary map), device */
+int ctg_synth_volume(uint64_t* labels, float* boundary, const int64_t* shape,
+                     int64_t z_offset, const int64_t* global_shape, int cell,
+                     uint64_t seed, uint64_t label_offset, double noise_amp, void* stream);
+int ctg_synth_affinities(const float* boundary, float* affs, const int64_t* shape,
+                         int n_channels, const int32_t* offsets, void* stream);
+
+/* profiling: per-phase device milliseconds of the last ctg_rag_features call
+ * (HIP events on the call's stream): [0] face scan, [1] key pack, [2] sort,
+ * [3] segment, [4] reduce+finalize, [5] nodes, [6] total */
+int ctg_set_profiling(int on);
+int ctg_last_timings(double* ms, int n);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CTG_H_ */

@@ -1,0 +1,71 @@
+"""ctypes wrapper of oracle/libctg_oracle.so (scalar C restatement).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/ and bench.py's cpu_baseline leg.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_lib = None
+
+
+def load():
+    global _lib
+    if _lib is None:
+        path = os.path.join(_HERE, 'libctg_oracle.so')
+        if not os.path.exists(path):
+            import subprocess
+            subprocess.check_call(['make', '-C', _HERE, '-s'])
+        lib = ctypes.CDLL(path)
+        vp = ctypes.c_void_p
+        lib.ctgo_features.restype = ctypes.c_int
+        lib.ctgo_features.argtypes = [vp, vp, ctypes.c_int, ctypes.c_int, vp, ctypes.c_int64, ctypes.c_int64,
+                                      ctypes.c_int64, vp, ctypes.c_int, ctypes.c_double, ctypes.c_double,
+                                      ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(vp), ctypes.POINTER(vp)]
+        lib.ctgo_free.argtypes = [vp]
+        lib.ctgo_free.restype = None
+        _lib = lib
+    return _lib
+
+
+def features(labels, data=None, offsets=None, own_begin=None, ignore_label=False, lo=0.0, hi=1.0):
+    """Returns (edges (E,2) uint64, features (E,10) float64)."""
+    lib = load()
+    labels = np.ascontiguousarray(labels, dtype=np.uint64)
+    Z, Y, X = labels.shape
+    mode = 0
+    dptr = None
+    optr = None
+    n_ch = 0
+    off = None
+    if data is not None:
+        if data.dtype == np.uint8:
+            data = data.astype(np.float32) / np.float32(255)
+        data = np.ascontiguousarray(data, dtype=np.float32)
+        dptr = data.ctypes.data_as(ctypes.c_void_p)
+        if offsets is not None:
+            mode = 2
+            off = np.ascontiguousarray(np.asarray(offsets, dtype=np.int32).reshape(-1, 3))
+            n_ch = off.shape[0]
+            optr = off.ctypes.data_as(ctypes.c_void_p)
+        else:
+            mode = 1
+    own = (ctypes.c_int64 * 3)(*own_begin) if own_begin is not None else None
+    n = ctypes.c_int64()
+    ep = ctypes.c_void_p()
+    fp = ctypes.c_void_p()
+    rc = lib.ctgo_features(labels.ctypes.data_as(ctypes.c_void_p), dptr, mode, n_ch, optr, Z, Y, X, own,
+                           int(bool(ignore_label)), float(lo), float(hi), ctypes.byref(n), ctypes.byref(ep),
+                           ctypes.byref(fp))
+    if rc != 0:
+        raise MemoryError('ctgo_features failed')
+    E = n.value
+    edges = np.ctypeslib.as_array(ctypes.cast(ep, ctypes.POINTER(ctypes.c_uint64)), shape=(max(E, 1) * 2,))
+    edges = edges[:2 * E].reshape(E, 2).copy()
+    feats = np.ctypeslib.as_array(ctypes.cast(fp, ctypes.POINTER(ctypes.c_double)), shape=(max(E, 1) * 10,))
+    feats = feats[:10 * E].reshape(E, 10).copy()
+    lib.ctgo_free(ep)
+    lib.ctgo_free(fp)
+    return edges, feats
