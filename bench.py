@@ -1,0 +1,200 @@
+#!/usr/bin/env python
+"""Throughput of the RAG + edge-feature hot path on MI355X.
+
+Metric (BASELINE.json): Gvoxels/s for RAG + boundary edge features, and the
+fraction of the HBM roofline.  One *step* = one pass of the hot path over a
+resident synthetic volume: face scan (labels uint64 + float32 boundary map in
+HBM) -> per-tile edge records -> radix sort -> per-edge reduction -> sorted
+(E,2) edge table, node list and (E,10) float64 feature table in HBM.
+
+N=1: BASELINE.json configs[1], 512^3 Voronoi supervoxels (cell 10, ~1e6
+edges) + boundary map.  N>1 (torch.distributed.run, one rank per GPU): weak
+scaling, each rank owns a 512^3 z-slab of a (512N)x512x512 volume (+1 halo
+plane), builds its partial edge table and the ranks combine them over RCCL
+(cluster_tools_amd/dist.py).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E peak, GB/s (MI355X_MICROARCH.md)
+EDGE_BYTES = 96                # 16 B (u,v) + 10 x float64 features
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument('--gpus', type=int, default=1)
+    p.add_argument('--steps', type=int, default=10)
+    p.add_argument('--warmup', type=int, default=3)
+    p.add_argument('--size', type=int, default=512, help='per-GPU cube edge (voxels)')
+    p.add_argument('--cell', type=int, default=10)
+    p.add_argument('--seed', type=int, default=0)
+    p.add_argument('--cpu-baseline-planes', type=int, default=96,
+                   help='z-planes of the per-GPU volume timed with the C oracle (0 = skip)')
+    p.add_argument('--no-cpu-baseline', action='store_true')
+    return p.parse_args()
+
+
+def pmc_traffic_per_launch():
+    """HBM bytes per face-scan launch from the committed rocprofv3 PMC summary
+    (profiles/*/pmc_summary.json, written by tools/pmc_summary.py), or None."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, 'profiles', '*', 'pmc_summary.json')))
+    for f in reversed(files):
+        try:
+            with open(f) as fh:
+                d = json.load(fh)
+            v = d.get('scan_hbm_bytes_per_launch')
+            if v:
+                return float(v), os.path.relpath(f, ROOT)
+        except Exception:
+            continue
+    return None, None
+
+
+def cpu_baseline(labels_t, bnd_t, planes):
+    """C oracle (scalar port, 1 thread) on the first ``planes`` z-planes."""
+    from oracle import c_oracle
+    lab = labels_t[:planes].cpu().numpy().view(np.uint64)
+    bnd = bnd_t[:planes].cpu().numpy()
+    c_oracle.features(lab[:4], bnd[:4])  # load / warm
+    t0 = time.perf_counter()
+    e, f = c_oracle.features(lab, bnd)
+    dt = time.perf_counter() - t0
+    return lab.size / dt / 1e9, dict(sample='%dx%dx%d z-slab of the same volume (%d voxels, %d edges)'
+                                     % (lab.shape + (lab.size, e.shape[0])), seconds=dt)
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    if args.gpus != world and world > 1:
+        print('warning: --gpus %d but WORLD_SIZE %d' % (args.gpus, world), file=sys.stderr)
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+
+    from cluster_tools_amd import rag
+    from cluster_tools_amd import _lib
+
+    _lib.init_device(local)
+    S = args.size
+    shape = (S, S, S)
+    gshape = (S * world, S, S)
+    halo = 1 if rank > 0 else 0
+    # rank r owns z in [r*S, (r+1)*S) and reads the plane below as halo
+    lab, bnd = rag.synth_volume((S + halo, S, S), cell=args.cell, seed=args.seed, z_offset=rank * S - halo,
+                                global_shape=gshape)
+    torch.cuda.synchronize()
+    own = (halo, 0, 0)
+
+    if world > 1:
+        from cluster_tools_amd import dist as cdist
+        step_fn = lambda: cdist.rag_features_distributed(lab, bnd, own_begin=own)  # noqa: E731
+    else:
+        step_fn = lambda: rag.rag_features_handle(lab, bnd, own_begin=own)  # noqa: E731
+
+    res = None
+    for _ in range(args.warmup):
+        if res is not None:
+            res.free()
+        res = step_fn()
+    torch.cuda.synchronize()
+    rag.set_profiling(True)
+    scan_ms = []
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        if res is not None:
+            res.free()
+        res = step_fn()
+        scan_ms.append(rag.last_timings()['scan'])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    rag.set_profiling(False)
+    elapsed = t1 - t0
+    if world > 1:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device='cuda')
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    n_edges_local = res.n_edges
+    n_rec, n_direct = res.info()
+    timings = rag.last_timings()
+
+    V = S ** 3                                # owned voxels per rank
+    total_vox = V * world
+    ms_step = elapsed / args.steps * 1e3
+    value = total_vox / (elapsed / args.steps) / 1e9
+    n_edges = n_edges_local
+    if world > 1:
+        te = torch.tensor([n_edges_local], dtype=torch.int64, device='cuda')
+        dist.all_reduce(te)
+        n_edges = int(te.item())
+
+    # roofline of the dominant kernel (face scan): algorithmic bytes per launch
+    # = voxels it scans x (8 B label + 4 B boundary), halo plane excluded
+    scan_avg_ms = float(np.mean(scan_ms))
+    scan_bytes = V * 12
+    achieved = scan_bytes / (scan_avg_ms * 1e-3) / 1e9
+    traffic, traffic_src = pmc_traffic_per_launch()
+    step_bytes = total_vox * 12 + n_edges * EDGE_BYTES
+
+    line = None
+    if rank == 0:
+        cpu = None
+        if not args.no_cpu_baseline and args.cpu_baseline_planes > 0 and world == 1:
+            v, info = cpu_baseline(lab, bnd, min(args.cpu_baseline_planes, S))
+            cpu = {'value': round(v, 6), 'unit': 'Gvoxels/s', 'cores': 1, 'kind': 'port',
+                   'sample': info['sample'] + ', %.2f s, oracle/ctg_oracle.c scalar C restatement '
+                                              '(nifty reference not present on this host)' % info['seconds']}
+        line = {
+            'metric': 'Gvoxels/s RAG+edge features (boundary map, uint64 labels, float32)',
+            'value': round(value, 4),
+            'unit': 'Gvoxels/s',
+            'n_gpus': world,
+            'steps': args.steps,
+            'warmup': args.warmup,
+            'ms_per_step': round(ms_step, 4),
+            'higher_is_better': True,
+            'scaling': 'weak',
+            'vs_baseline': None,
+            'dtype': 'u64 labels / f32 samples / f64 stats',
+            'data': 'synthetic (jittered-grid Voronoi supervoxels + boundary map, generated in HBM)',
+            'config': {'workload': 'BASELINE configs[1]: %d^3 per GPU, cell %d, boundary map' % (S, args.cell),
+                       'volume': list(gshape), 'edges': n_edges, 'parallelism': 'z-slab x%d' % world},
+            'roofline': {'bound': 'hbm', 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+                         'frac': round(achieved / HBM_PEAK_GBS, 4),
+                         'traffic': traffic, 'kernel': 'k_face_scan',
+                         'kernel_ms': round(scan_avg_ms, 4), 'algorithmic_bytes': scan_bytes,
+                         'traffic_source': traffic_src},
+            'step_roofline_frac': round(step_bytes / (ms_step * 1e-3) / 1e9 / (HBM_PEAK_GBS * world), 4),
+            'phase_ms': {k: round(v, 4) for k, v in timings.items()},
+            'records': n_rec, 'direct_faces': n_direct,
+            'cpu_baseline': cpu,
+        }
+        print(json.dumps(line), flush=True)
+    res.free()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

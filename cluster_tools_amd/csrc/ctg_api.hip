@@ -28,6 +28,10 @@ hipError_t launch_compact(int64_t E, const uint32_t* keep, const uint32_t* pos, 
                           const ReduceOut& out, hipStream_t s);
 hipError_t launch_endpoints(int64_t E, const uint64_t* uniq, int nb, uint32_t* out, hipStream_t s);
 hipError_t launch_u32_to_u64(int64_t n, const uint32_t* in, uint64_t* out, hipStream_t s);
+hipError_t launch_mark_nodes(int64_t E, const uint64_t* uniq, int nb, uint32_t* bits, hipStream_t s);
+hipError_t launch_popc_words(int64_t W, const uint32_t* bits, uint32_t* cnt, hipStream_t s);
+hipError_t launch_bits_to_nodes(int64_t W, const uint32_t* bits, const uint32_t* off, uint64_t* nodes,
+                                hipStream_t s);
 hipError_t launch_find_edges(const uint64_t* ge, int64_t n, const uint64_t* q, int64_t m, int64_t* out,
                              hipStream_t s);
 hipError_t launch_synth(uint64_t* labels, float* boundary, const int64_t* shape, int64_t z_offset,
@@ -273,7 +277,33 @@ static hipError_t reduce_records(Workspace& w, const ReduceJob& J, hipStream_t s
     res->stat_sums = O.wsums;
 
     // nodes = unique endpoints of every unique key (before filtering)
-    if (E_all > 0) {
+    if (E_all > 0 && J.max_v < (1ull << 30)) {
+        // bitmap over [0, max label]: one pass over the sorted key table
+        const int64_t W = (int64_t)(J.max_v >> 5) + 1;
+        uint32_t* bits = (uint32_t*)dalloc(W * 4);
+        uint32_t* cnt = (uint32_t*)dalloc(W * 4);
+        uint32_t* off = (uint32_t*)dalloc(W * 4);
+        if (!bits || !cnt || !off) return hipErrorOutOfMemory;
+        e = hipMemsetAsync(bits, 0, W * 4, s);
+        if (e != hipSuccess) return e;
+        e = launch_mark_nodes(E_all, w.uniq, nb, bits, s);
+        if (e != hipSuccess) return e;
+        e = launch_popc_words(W, bits, cnt, s);
+        if (e != hipSuccess) return e;
+        ROCPRIM_CALL(w, rocprim::exclusive_scan(t, tbytes, cnt, off, 0u, (size_t)W, rocprim::plus<uint32_t>(), s));
+        e = hipMemcpyAsync(w.small_host + 1, off + (W - 1), 4, hipMemcpyDeviceToHost, s);
+        if (e != hipSuccess) return e;
+        e = hipMemcpyAsync(w.small_host + 2, cnt + (W - 1), 4, hipMemcpyDeviceToHost, s);
+        if (e != hipSuccess) return e;
+        e = hipStreamSynchronize(s);
+        if (e != hipSuccess) return e;
+        const int64_t N = (int64_t)w.small_host[1] + w.small_host[2];
+        res->nodes = (uint64_t*)dalloc(std::max<int64_t>(N, 1) * 8);
+        e = launch_bits_to_nodes(W, bits, off, res->nodes, s);
+        if (e != hipSuccess) return e;
+        res->n_nodes = N;
+        dfree(bits); dfree(cnt); dfree(off);
+    } else if (E_all > 0) {
         uint32_t* ep = (uint32_t*)dalloc(E_all * 8);
         uint32_t* ep2 = (uint32_t*)dalloc(E_all * 8);
         uint32_t* nodes32 = (uint32_t*)dalloc(E_all * 8);
@@ -364,7 +394,8 @@ static int stage_in(Workspace& w, int slot, const void* src, size_t bytes, int m
 }
 
 int ctg_rag_features(const void* labels, int label_bits, const void* data, int data_kind, int n_channels,
-                     const int32_t* offsets, const int64_t* shape, const int64_t* own_begin, int ignore_label,
+                     const int32_t* offsets, const int64_t* shape, const int64_t* own_begin,
+                     const int64_t* own_end, int ignore_label,
                      double hist_lo, double hist_hi, int keep_stats, int mem, void* stream, ctg_result** out) {
     if (!out || !shape || !labels) {
         set_error("ctg_rag_features: null argument");
@@ -388,8 +419,8 @@ int ctg_rag_features(const void* labels, int label_bits, const void* data, int d
         return CTG_ERR_ARG;
     }
     for (int k = 0; k < 3; ++k)
-        if (shape[k] < 0 || (own_begin && (own_begin[k] < 0))) {
-            set_error("ctg_rag_features: negative shape/own_begin");
+        if (shape[k] < 0 || (own_begin && (own_begin[k] < 0)) || (own_end && own_end[k] < 0)) {
+            set_error("ctg_rag_features: negative shape/own_begin/own_end");
             return CTG_ERR_ARG;
         }
     const int dev = cur_dev();
@@ -418,15 +449,27 @@ int ctg_rag_features(const void* labels, int label_bits, const void* data, int d
     for (int k = 0; k < 3; ++k) {
         P.shape[k] = shape[k];
         P.own_begin[k] = own_begin ? own_begin[k] : 0;
+        P.own_end[k] = own_end ? std::min(own_end[k], shape[k]) : shape[k];
     }
     P.scale = (double)NBINS / (hist_hi - hist_lo);
     P.offset = hist_lo;
-    // u16 histogram slots in the LDS table must not overflow within one tile:
-    // samples per entry per tile <= samples_per_voxel * 64 * 8 * tile_z < 65536
+    P.fast40 = (hist_lo == 0.0 && P.scale == 40.0) ? 1 : 0;
+    // A u16 histogram slot gains at most spv samples per voxel of one plane of
+    // the 64x32 tile cross-section; the scan flushes its LDS table before any
+    // entry could reach 65535 within the next plane.
     const int spv = P.n_channels > 0 ? std::max(P.n_channels, 3) : 6;
-    int tz = 65535 / (TILE_X * TILE_Y * spv);
-    tz = std::max(1, std::min(16, tz));
-    P.tile_z = tz;
+    P.hist_guard = (uint32_t)(65535 - spv * TILE_X * 32);
+    // planes per workgroup: deep tiles (fewer records), but >= ~1024 workgroups
+    {
+        const int64_t cols = ((shape[2] + TILE_X - 1) / TILE_X) * ((shape[1] + 31) / 32);
+        int tz = 64;
+        while (tz > 8 && cols * ((shape[0] + tz - 1) / tz) < 1024) tz /= 2;
+        P.tile_z = tz;
+    }
+    {
+        const char* ab = getenv("CTG_ABLATE");
+        P.ablate = ab ? atoi(ab) : 0;
+    }
 
     Ev ev{w, s};
     ev.mark(0);
@@ -483,7 +526,7 @@ int ctg_rag_features(const void* labels, int label_bits, const void* data, int d
     // single-label array: the owned origin voxel is the only node
     const int64_t o0 = own_begin ? own_begin[0] : 0, o1 = own_begin ? own_begin[1] : 0,
                   o2 = own_begin ? own_begin[2] : 0;
-    const bool has_owned = o0 < shape[0] && o1 < shape[1] && o2 < shape[2];
+    const bool has_owned = o0 < P.own_end[0] && o1 < P.own_end[1] && o2 < P.own_end[2];
     J.single_label_ptr = (label_bits == 64 && has_owned)
                              ? (const uint64_t*)dl + ((o0 * shape[1] + o1) * shape[2] + o2)
                              : nullptr;
@@ -662,6 +705,64 @@ int ctg_merge_stats(const uint64_t* keys, const double* sums, const uint32_t* re
     }
     if (e != hipSuccess) {
         set_error(std::string("ctg_merge_stats: ") + hipGetErrorString(e));
+        ctg_free(r);
+        return CTG_ERR_HIP;
+    }
+    *out = r;
+    return CTG_OK;
+}
+
+int ctg_unique_pairs(const uint64_t* pairs, int64_t n, int mem, void* stream, ctg_result** out) {
+    if (!out || n < 0 || (n > 0 && !pairs)) {
+        set_error("ctg_unique_pairs: bad arguments");
+        return CTG_ERR_ARG;
+    }
+    *out = nullptr;
+    const int dev = cur_dev();
+    Workspace& w = ws(dev);
+    CTG_CHECK(ws_init(w));
+    hipStream_t s = (hipStream_t)stream;
+    ctg_result* r = new ctg_result();
+    r->device = dev;
+    if (n == 0) {
+        r->edges = (uint64_t*)dalloc(16);
+        r->nodes = (uint64_t*)dalloc(8);
+        *out = r;
+        return CTG_OK;
+    }
+    uint64_t* dk = (uint64_t*)pairs;
+    if (mem == CTG_MEM_HOST) {
+        dk = (uint64_t*)dalloc(n * 16);
+        if (!dk) {
+            set_error("ctg_unique_pairs: out of device memory");
+            delete r;
+            return CTG_ERR_NOMEM;
+        }
+        CTG_CHECK(hipMemcpyAsync(dk, pairs, n * 16, hipMemcpyHostToDevice, s));
+    }
+    CTG_CHECK(hipMemsetAsync(w.counters, 0, sizeof(Counters), s));
+    CTG_CHECK(launch_max_pairs(n, dk, &w.counters->max_v, s));
+    CTG_CHECK(hipMemcpyAsync(w.counters_host, w.counters, sizeof(Counters), hipMemcpyDeviceToHost, s));
+    CTG_CHECK(hipStreamSynchronize(s));
+    if (w.counters_host->max_v >> 32) {
+        set_error("ctg_unique_pairs: labels >= 2^32 are not supported");
+        if (mem == CTG_MEM_HOST) dfree(dk);
+        delete r;
+        return CTG_ERR_UNSUPPORTED;
+    }
+    ReduceJob J{};
+    J.n = n;
+    J.pairs = dk;
+    J.stats = 0;
+    J.need_adj = 0;
+    J.max_v = w.counters_host->max_v;
+    J.scale = 1.0;
+    J.offset = 0.0;
+    hipError_t e = reduce_records(w, J, s, r);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (mem == CTG_MEM_HOST) dfree(dk);
+    if (e != hipSuccess) {
+        set_error(std::string("ctg_unique_pairs: ") + hipGetErrorString(e));
         ctg_free(r);
         return CTG_ERR_HIP;
     }

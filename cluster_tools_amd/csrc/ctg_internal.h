@@ -15,7 +15,7 @@ namespace ctg {
 // fixed geometry of the face-scan tiles and the LDS edge table
 // ---------------------------------------------------------------------------
 constexpr int WAVE = 64;
-constexpr int SCAN_THREADS = 256;      // 4 waves per workgroup
+constexpr int SCAN_THREADS = 512;      // 8 waves per workgroup
 constexpr int TILE_X = 64;             // one wave row
 constexpr int TILE_Y = 8;
 constexpr int TABLE_CAP = 512;         // LDS edge-table entries (power of two)
@@ -78,9 +78,13 @@ struct ScanParams {
     int offsets[CTG_MAX_CHANNELS][3];
     int64_t shape[3];
     int64_t own_begin[3];
+    int64_t own_end[3];
     double scale, offset;      // histogram mapping
     double u8_scale;           // uint8 -> float factor (1/255)
-    int tile_z;
+    int tile_z;                // z-planes per workgroup
+    uint32_t hist_guard;       // flush before a u16 histogram slot can wrap
+    int fast40;                // histogram range [0,1) x 40 bins: exact f32 binning
+    int ablate;                // diagnostic: 8 loads only, 16 no per-plane barrier
 };
 
 struct Counters {               // device-side counters, zeroed per call

@@ -47,54 +47,66 @@ __global__ void k_max_pairs(int64_t n, const uint64_t* __restrict__ uv, unsigned
 // ---------------------------------------------------------------------------
 // vigra computeStandardQuantiles as a single streaming walk over the bins
 // ---------------------------------------------------------------------------
-struct QuantileWalk {
-    static constexpr int NQ = 7;
-    double count, scale, inv_scale, offset;
-    double res[NQ];
-    int q, qend;
-    double qcount;
-    bool have_prev, have_pend;
-    double prev_kp, prev_ch, pend_kp, pend_ch;
+// The keypoints (mapped value, cumulative count) are generated in order; the
+// last generated point is held back one step because vigra replaces the final
+// keypoint by (mapped max, count) when there are no right outliers.  Each
+// interior quantile q (0.1 .. 0.9) is interpolated on the first segment with
+// cum(a) < q*count <= cum(b) and written straight to out[q] (global memory:
+// no dynamically indexed register arrays, no scratch).
+__device__ __forceinline__ double qv5(int i) {
+    return i == 0 ? 0.1 : i == 1 ? 0.25 : i == 2 ? 0.5 : i == 3 ? 0.75 : 0.9;
+}
 
-    __device__ __forceinline__ static double qv(int i) {
-        // 0.0 and 1.0 handled exactly (min/max), the rest by interpolation
-        return i == 1 ? 0.1 : i == 2 ? 0.25 : i == 3 ? 0.5 : i == 4 ? 0.75 : i == 5 ? 0.9 : (i == 0 ? 0.0 : 1.0);
-    }
-    __device__ void init(double cnt, double sc, double off) {
-        count = cnt;
-        scale = sc;
-        inv_scale = 1.0 / sc;
-        offset = off;
-        for (int i = 0; i < NQ; ++i) res[i] = 0.0;
-        q = 1;  // quantile 0.0 -> minimum
-        qend = NQ - 1;  // quantile 1.0 -> maximum
-        qcount = count * qv(q);
-        have_prev = have_pend = false;
-    }
-    __device__ void consume(double kp, double ch) {
+__device__ void vigra_quantiles(const uint32_t* __restrict__ hl, double count, double vmin, double vmax,
+                                double scale, double offset, double* __restrict__ out) {
+    const double inv = 1.0 / scale;
+    int q = 0;
+    double qc = count * qv5(0);
+    bool have_prev = false, have_pend = false;
+    double pkp = 0.0, pch = 0.0, kp_pend = 0.0, ch_pend = 0.0;
+    auto consume = [&](double kp, double ch) {
         if (!have_prev) {
-            prev_kp = kp;
-            prev_ch = ch;
+            pkp = kp;
+            pch = ch;
             have_prev = true;
             return;
         }
-        while (q < qend && prev_ch < qcount && ch >= qcount) {
-            double t = (qcount - prev_ch) / (ch - prev_ch) * (kp - prev_kp);
-            res[q] = inv_scale * (t + prev_kp) + offset;
+        while (q < 5 && pch < qc && ch >= qc) {
+            const double t = (qc - pch) / (ch - pch) * (kp - pkp);
+            out[q] = inv * (t + pkp) + offset;
             ++q;
-            qcount = count * qv(q);
+            qc = count * qv5(q);
         }
-        prev_kp = kp;
-        prev_ch = ch;
-    }
-    __device__ void gen(double kp, double ch) {
-        if (have_pend) consume(pend_kp, pend_ch);
-        pend_kp = kp;
-        pend_ch = ch;
+        pkp = kp;
+        pch = ch;
+    };
+    auto gen = [&](double kp, double ch) {
+        if (have_pend) consume(kp_pend, ch_pend);
+        kp_pend = kp;
+        ch_pend = ch;
         have_pend = true;
+    };
+    gen(scale * (vmin - offset), 0.0);
+    const double left = (double)hl[0], right = (double)hl[NSLOTS - 1];
+    if (left > 0.0) gen(0.0, left);
+    double cum = left;
+#pragma unroll 1
+    for (int k = 0; k < NBINS; ++k) {
+        const uint32_t hk = hl[k + 1];
+        if (hk > 0) {
+            if (kp_pend <= (double)k) gen((double)k, cum);
+            cum += (double)hk;
+            gen((double)(k + 1), cum);
+        }
     }
-    __device__ double last_kp() const { return pend_kp; }
-};
+    if (right > 0.0) {
+        if (kp_pend != (double)NBINS) gen((double)NBINS, cum);
+        gen(scale * (vmax - offset), count);
+        consume(kp_pend, ch_pend);
+    } else {
+        consume(scale * (vmax - offset), count);  // replaces the last keypoint
+    }
+}
 
 template <bool WIDE>
 __device__ __forceinline__ void load_record(const RecordBuf& R, uint32_t i, uint32_t (&h)[NSLOTS], uint32_t& cnt,
@@ -190,48 +202,29 @@ __global__ __launch_bounds__(256) void k_reduce_edges(int64_t E, const uint64_t*
             O.wsums[e] = make_double2(sum, sq);
         }
         if (!O.feats) return;
-        double f[N_FEATURES];
-#pragma unroll
-        for (int j = 0; j < N_FEATURES; ++j) f[j] = 0.0;
-        if (cnt > 0) {
-            const double c = (double)cnt;
-            const double mean = sum / c;
-            double var = (sq - sum * mean) / c;
-            if (var < 0.0) var = 0.0;
-            const double vmin = (double)ord2f(mn), vmax = (double)ord2f(mx);
-            QuantileWalk W;
-            W.init(c, scale, offset);
-            const double left = (double)h[0], right = (double)h[NSLOTS - 1];
-            W.gen(scale * (vmin - offset), 0.0);
-            if (left > 0.0) W.gen(0.0, left);
-            double cum = left;
-#pragma unroll
-            for (int k = 0; k < NBINS; ++k) {
-                const uint32_t hk = h[k + 1];
-                if (hk > 0) {
-                    if (W.last_kp() <= (double)k) W.gen((double)k, cum);
-                    cum += (double)hk;
-                    W.gen((double)(k + 1), cum);
-                }
-            }
-            if (right > 0.0) {
-                if (W.last_kp() != (double)NBINS) W.gen((double)NBINS, cum);
-                W.gen(scale * (vmax - offset), c);
-                W.consume(W.pend_kp, W.pend_ch);
-            } else {
-                W.consume(scale * (vmax - offset), c);  // replaces the last keypoint
-            }
-            f[0] = mean;
-            f[1] = var;
-            f[2] = vmin;
-#pragma unroll
-            for (int j = 1; j < 6; ++j) f[2 + j] = W.res[j];
-            f[8] = vmax;
-            f[9] = c;
-        }
         double* o = O.feats + (size_t)e * N_FEATURES;
+        if (cnt == 0) {
 #pragma unroll
-        for (int j = 0; j < N_FEATURES; ++j) o[j] = f[j];
+            for (int j = 0; j < N_FEATURES; ++j) o[j] = 0.0;
+            return;
+        }
+        const double c = (double)cnt;
+        const double mean = sum / c;
+        double var = (sq - sum * mean) / c;
+        if (var < 0.0) var = 0.0;
+        const double vmin = (double)ord2f(mn), vmax = (double)ord2f(mx);
+        // the walk reads the bins back from this thread's LDS row
+        __shared__ uint32_t H[256][NSLOTS + 1];
+        uint32_t* hl = H[threadIdx.x];
+#pragma unroll
+        for (int j = 0; j < NSLOTS; ++j) hl[j] = h[j];
+        o[0] = mean;
+        o[1] = var;
+        o[2] = vmin;
+        o[3] = o[4] = o[5] = o[6] = o[7] = 0.0;
+        vigra_quantiles(hl, c, vmin, vmax, scale, offset, o + 3);
+        o[8] = vmax;
+        o[9] = c;
     }
 }
 
@@ -259,6 +252,50 @@ __global__ void k_endpoints(int64_t E, const uint64_t* __restrict__ uniq, int nb
     const uint64_t sk = uniq[e];
     out[2 * e] = (uint32_t)(sk >> nb);
     out[2 * e + 1] = (uint32_t)(sk & ((1ull << nb) - 1ull));
+}
+
+// nodes as a bitmap over [0, max label]: u is sorted in the key table, so only
+// run heads mark it; every v marks its bit
+__global__ void k_mark_nodes(int64_t E, const uint64_t* __restrict__ uniq, int nb, uint32_t* __restrict__ bits) {
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= E) return;
+    const uint64_t sk = uniq[e];
+    const uint32_t u = (uint32_t)(sk >> nb), v = (uint32_t)(sk & ((1ull << nb) - 1ull));
+    if (e == 0 || (uint32_t)(uniq[e - 1] >> nb) != u) atomicOr(&bits[u >> 5], 1u << (u & 31));
+    atomicOr(&bits[v >> 5], 1u << (v & 31));
+}
+
+__global__ void k_popc_words(int64_t W, const uint32_t* __restrict__ bits, uint32_t* __restrict__ cnt) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < W) cnt[i] = __popc(bits[i]);
+}
+
+__global__ void k_bits_to_nodes(int64_t W, const uint32_t* __restrict__ bits, const uint32_t* __restrict__ off,
+                                uint64_t* __restrict__ nodes) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= W) return;
+    uint32_t b = bits[i];
+    uint32_t o = off[i];
+    while (b) {
+        const int k = __ffs(b) - 1;
+        nodes[o++] = (uint64_t)(i * 32 + k);
+        b &= b - 1;
+    }
+}
+
+hipError_t launch_mark_nodes(int64_t E, const uint64_t* uniq, int nb, uint32_t* bits, hipStream_t s) {
+    if (E == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_mark_nodes, dim3((unsigned)((E + 255) / 256)), dim3(256), 0, s, E, uniq, nb, bits);
+    return hipGetLastError();
+}
+hipError_t launch_popc_words(int64_t W, const uint32_t* bits, uint32_t* cnt, hipStream_t s) {
+    hipLaunchKernelGGL(k_popc_words, dim3((unsigned)((W + 255) / 256)), dim3(256), 0, s, W, bits, cnt);
+    return hipGetLastError();
+}
+hipError_t launch_bits_to_nodes(int64_t W, const uint32_t* bits, const uint32_t* off, uint64_t* nodes,
+                                hipStream_t s) {
+    hipLaunchKernelGGL(k_bits_to_nodes, dim3((unsigned)((W + 255) / 256)), dim3(256), 0, s, W, bits, off, nodes);
+    return hipGetLastError();
 }
 
 __global__ void k_u32_to_u64(int64_t n, const uint32_t* __restrict__ in, uint64_t* __restrict__ out) {

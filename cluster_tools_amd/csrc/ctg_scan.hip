@@ -1,18 +1,24 @@
 // Face scan: the O(V) hot loop of the RAG + edge-feature path (gfx950).
 //
-// One workgroup (4 waves) owns a tile of 64 (x) x 8 (y) x tile_z (z) voxels.
-// A wave walks one z-plane of the tile row by row (lane = x), carrying the
-// y-neighbour row in registers, so every label/value is read from HBM once;
-// the z-neighbour row and the lane-63 x-neighbour come from L2.  Every
+// One workgroup (8 waves) owns a tile of 64 (x) x 32 (y) x tile_z (z) voxels.
+// Each wave holds 4 rows (+ the y-halo row) of one z-plane in registers
+// (lane = x) and walks z with the next plane's loads in flight while it works
+// on the current one, so every label/value is read from HBM once.  Every
 // boundary face (p, p+e_a) with differing labels is folded into an LDS
 // open-addressing edge table keyed by (u<<32)|v that holds, per edge, the
 // sample count, f64 sum and sum of squares, order-preserving min/max and the
 // 42-slot vigra histogram (u16 slots packed in u32 words).  The table is
-// flushed to HBM as one record per (tile, edge) when it is half full and at the
-// end of the tile, so HBM sees ~E*(tile surface factor) records instead of one
-// entry per face.  Replaces the per-face std::set / findEdge loop of
-// nifty.distributed (called at graph/initial_sub_graphs.py:124-129 and
-// features/block_edge_features.py:127-145).
+// flushed to HBM as one record per (tile, edge) when it is half full, when a
+// u16 slot could wrap within the next plane, and at the end of the tile.
+//
+// Per-face work is kept off the LDS critical path:
+//  * per-lane caches hold the last key of each face axis (x and z faces repeat
+//    along y, y faces along z), with x/z statistics pending in registers;
+//  * the keys of a row batch are resolved together: every cache miss reads its
+//    2-slot home bucket with one 16-byte LDS load, all issued back to back, and
+//    only keys missing from their home bucket walk the probe/insert loop.
+// Replaces the per-face std::set / findEdge loop of nifty.distributed (called
+// at graph/initial_sub_graphs.py:124-129 and features/block_edge_features.py:127-145).
 #include "ctg_internal.h"
 
 namespace ctg {
@@ -41,10 +47,14 @@ __device__ __forceinline__ void entry_reset(Table& T, int e) {
     T.w[e][23] = ORD_NEG_INF;
 }
 
+// home bucket of a key: two slots (even, odd) read by one ds_read_b128
+__device__ __forceinline__ uint32_t home_bucket(uint64_t key) { return hash_key(key) & (TABLE_CAP - 2); }
+
+// linear probing from the home bucket; returns the slot or -1 when full
 __device__ __forceinline__ int table_insert(Table& T, uint64_t key) {
-    uint32_t h = hash_key(key) & (TABLE_CAP - 1);
+    uint32_t h = home_bucket(key);
 #pragma unroll 1
-    for (int i = 0; i < 48; ++i) {
+    for (int i = 0; i < 64; ++i) {
         uint64_t cur = __hip_atomic_load(&T.key[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         if (cur == key) return (int)h;
         if (cur == EMPTY_KEY) {
@@ -113,37 +123,43 @@ __device__ void table_flush(Table& T, RecordBuf R, Counters* C) {
 
 // a face or affinity sample that found no room in the LDS table goes straight
 // to HBM as a one-sample (or two-sample) record
-__device__ void emit_direct(RecordBuf R, Counters* C, uint64_t key, int nsamp, float a, float b,
-                            double scale, double offset, uint32_t flag, bool with_stats) {
+__device__ __noinline__ void emit_direct(RecordBuf R, Counters* C, uint64_t key, int nsamp, float a, float b,
+                                         double scale, double offset, uint32_t flag, bool with_stats) {
     unsigned long long i = atomicAdd(&C->n_records, 1ull);
     atomicAdd(&C->n_direct, 1ull);
     atomicMax(&C->max_v, (unsigned long long)(key & 0xFFFFFFFFull));
     if (i >= (unsigned long long)R.cap) return;
     R.key[i] = key;
     if (!with_stats) return;
-    uint32_t row[NREC_WORDS];
-#pragma unroll
-    for (int j = 0; j < NREC_WORDS; ++j) row[j] = 0;
-    double s = 0.0, q = 0.0;
+    uint32_t w21 = 0;
     uint32_t mn = ORD_POS_INF, mx = ORD_NEG_INF;
+    double s = 0.0, q = 0.0;
+    int sa = -1, sb = -1;
     if (nsamp >= 1) {
-        int sa = hist_slot((double)a, scale, offset);
-        row[sa >> 1] += 1u << ((sa & 1) * 16);
-        s += (double)a; q += (double)a * (double)a;
-        mn = min(mn, f2ord(a)); mx = max(mx, f2ord(a));
+        sa = hist_slot((double)a, scale, offset);
+        s += (double)a;
+        q += (double)a * (double)a;
+        mn = min(mn, f2ord(a));
+        mx = max(mx, f2ord(a));
     }
     if (nsamp >= 2) {
-        int sb = hist_slot((double)b, scale, offset);
-        row[sb >> 1] += 1u << ((sb & 1) * 16);
-        s += (double)b; q += (double)b * (double)b;
-        mn = min(mn, f2ord(b)); mx = max(mx, f2ord(b));
+        sb = hist_slot((double)b, scale, offset);
+        s += (double)b;
+        q += (double)b * (double)b;
+        mn = min(mn, f2ord(b));
+        mx = max(mx, f2ord(b));
     }
-    row[21] = (uint32_t)nsamp | flag;
-    row[22] = mn;
-    row[23] = mx;
+    w21 = (uint32_t)nsamp | flag;
     R.sums[i] = make_double2(s, q);
-#pragma unroll
-    for (int j = 0; j < NREC_WORDS; ++j) R.hist[i * NREC_WORDS + j] = row[j];
+    for (int j = 0; j < HWORDS; ++j) {
+        uint32_t v = 0;
+        if (sa >= 0 && (sa >> 1) == j) v += 1u << ((sa & 1) * 16);
+        if (sb >= 0 && (sb >> 1) == j) v += 1u << ((sb & 1) * 16);
+        R.hist[i * NREC_WORDS + j] = v;
+    }
+    R.hist[i * NREC_WORDS + 21] = w21;
+    R.hist[i * NREC_WORDS + 22] = mn;
+    R.hist[i * NREC_WORDS + 23] = mx;
 }
 
 template <typename DataT>
@@ -155,48 +171,131 @@ __device__ __forceinline__ float load_val(const DataT* p, int64_t i) {
     }
 }
 
-template <int MODE>
-__device__ __forceinline__ void add_samples(Table& T, int s, int nsamp, float a, float b,
-                                            double scale, double offset) {
-    double sum = (double)a, sq = (double)a * (double)a;
-    float mn = a, mx = a;
-    if (nsamp == 2) {
-        sum += (double)b;
-        sq += (double)b * (double)b;
-        mn = fminf(a, b);
-        mx = fmaxf(a, b);
-    }
-    atomicAdd(&T.w[s][21], (uint32_t)nsamp);
-    atomicAdd(&T.sum[s], sum);
-    atomicAdd(&T.sq[s], sq);
-    atomicMin(&T.w[s][22], f2ord(mn));
-    atomicMax(&T.w[s][23], f2ord(mx));
-    int sa = hist_slot((double)a, scale, offset);
-    atomicAdd(&T.w[s][sa >> 1], 1u << ((sa & 1) * 16));
-    if (nsamp == 2) {
-        int sb = hist_slot((double)b, scale, offset);
-        atomicAdd(&T.w[s][sb >> 1], 1u << ((sb & 1) * 16));
+template <typename LabelT>
+__device__ __forceinline__ LabelT shfl_lane(LabelT v, int src) {
+    if constexpr (sizeof(LabelT) == 8) {
+        uint32_t lo = __shfl((uint32_t)v, src, WAVE), hi = __shfl((uint32_t)(v >> 32), src, WAVE);
+        return ((LabelT)hi << 32) | lo;
+    } else {
+        return (LabelT)__shfl((uint32_t)v, src, WAVE);
     }
 }
 
 template <typename LabelT>
 __device__ __forceinline__ LabelT shfl_down1(LabelT v) {
     if constexpr (sizeof(LabelT) == 8) {
-        uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
-        lo = __shfl_down(lo, 1, WAVE);
-        hi = __shfl_down(hi, 1, WAVE);
+        uint32_t lo = __shfl_down((uint32_t)v, 1, WAVE), hi = __shfl_down((uint32_t)(v >> 32), 1, WAVE);
         return ((LabelT)hi << 32) | lo;
     } else {
         return (LabelT)__shfl_down((uint32_t)v, 1, WAVE);
     }
 }
 
+// vigra binning of one sample.  fast40: range [0,1) with 40 bins, where
+// m = 40*x is computed exactly as p + e (two-product with an f32 FMA): the
+// slot equals the double-precision rule of hist_slot for every float x >= 0.
+__device__ __forceinline__ int sample_slot(float x, bool fast40, double scale, double offset) {
+    if (fast40 && x >= 0.f) {
+        const float p = x * 40.0f;
+        const float e = __builtin_fmaf(x, 40.0f, -p);
+        // m == 40 -> bin 39 (slot 40); m in (39,40) -> slot 40; m > 40 -> right outlier
+        if (p >= 40.0f) return (p == 40.0f && e <= 0.0f) ? NBINS : NBINS + 1;
+        float fl = floorf(p);
+        if (fl == p && e < 0.0f) fl -= 1.0f;
+        return (int)fl + 1;
+    }
+    return hist_slot((double)x, scale, offset);
+}
+
+__device__ __forceinline__ void hist_add(Table& T, int s, int k) {
+    atomicAdd(&T.w[s][k >> 1], 1u << ((k & 1) * 16));
+}
+
+constexpr int ROWS = 4;                                   // y rows per wave, held in registers
+constexpr int WAVES = SCAN_THREADS / WAVE;                // 8
+constexpr int WG_ROWS = ROWS * WAVES;                     // 32 = tile y extent
+constexpr uint32_t MARK_ADJ = 0xFFFFFFFFu;                // stage entry: nearest-neighbour face, no sample
+constexpr uint32_t MARK_ONE = 0xFFFFFFFEu;                // stage entry: one affinity sample in .z
+
+template <typename LabelT>
+__device__ __forceinline__ bool make_key(LabelT a, LabelT b, uint64_t& key, bool& ovf) {
+    const LabelT u = a < b ? a : b;
+    const LabelT v = a < b ? b : a;
+    if constexpr (sizeof(LabelT) == 8) {
+        if (v >> 32) {
+            ovf = true;
+            return false;
+        }
+    }
+    key = ((uint64_t)u << 32) | (uint64_t)v;
+    return true;
+}
+
+// Compacted face stream.  Each site (one row of one face axis) contributes
+// only its active lanes: they append (key, sample a, sample b) to the wave's
+// LDS stage at ballot/mbcnt positions; once the next site would overflow the
+// 64 entries, the wave takes the staged faces one per lane and folds them into
+// the edge table (home-bucket probe, statistics atomics, histogram).  Every
+// lane of a batch carries a face, instead of ~1 in 10 lanes of a site.
+template <int MODE>
+__device__ __forceinline__ void fold_batch(Table& T, const uint4* __restrict__ stage, int nb, int lane, RecordBuf R,
+                                           Counters* C, bool fast40, double scale, double offset) {
+    constexpr bool BND = MODE == MODE_BOUNDARY;
+    constexpr bool AFF = MODE == MODE_AFFINITY;
+    constexpr bool STATS = MODE != MODE_GRAPH;
+    if (lane >= nb) return;
+    const uint4 e = stage[lane];
+    const uint64_t key = ((uint64_t)e.y << 32) | e.x;
+    const uint32_t h = home_bucket(key);
+    const uint4 bk = *reinterpret_cast<const uint4*>(&T.key[h]);
+    const uint64_t k0 = ((uint64_t)bk.y << 32) | bk.x;
+    const uint64_t k1 = ((uint64_t)bk.w << 32) | bk.z;
+    const int s = k0 == key ? (int)h : (k1 == key ? (int)h + 1 : table_insert(T, key));
+    const float a = __uint_as_float(e.z), b = __uint_as_float(e.w);
+    if (s < 0) {
+        if constexpr (BND) emit_direct(R, C, key, 2, a, b, scale, offset, 0u, true);
+        if constexpr (AFF) {
+            if (e.w == MARK_ADJ) emit_direct(R, C, key, 0, 0.f, 0.f, scale, offset, ADJ_FLAG, true);
+            else emit_direct(R, C, key, 1, a, 0.f, scale, offset, 0u, true);
+        }
+        if constexpr (!STATS) emit_direct(R, C, key, 0, 0.f, 0.f, scale, offset, 0u, false);
+        return;
+    }
+    if constexpr (BND) {
+        atomicAdd(&T.w[s][21], 2u);
+        atomicAdd(&T.sum[s], (double)a + (double)b);
+        atomicAdd(&T.sq[s], (double)a * (double)a + (double)b * (double)b);
+        atomicMin(&T.w[s][22], f2ord(fminf(a, b)));
+        atomicMax(&T.w[s][23], f2ord(fmaxf(a, b)));
+        hist_add(T, s, sample_slot(a, fast40, scale, offset));
+        hist_add(T, s, sample_slot(b, fast40, scale, offset));
+    }
+    if constexpr (AFF) {
+        if (e.w == MARK_ADJ) {
+            atomicOr(&T.w[s][21], ADJ_FLAG);
+        } else {
+            atomicAdd(&T.w[s][21], 1u);
+            atomicAdd(&T.sum[s], (double)a);
+            atomicAdd(&T.sq[s], (double)a * (double)a);
+            atomicMin(&T.w[s][22], f2ord(a));
+            atomicMax(&T.w[s][23], f2ord(a));
+            hist_add(T, s, sample_slot(a, fast40, scale, offset));
+        }
+    }
+}
+
 template <typename LabelT, typename DataT, int MODE>
-__global__ __launch_bounds__(SCAN_THREADS) void k_face_scan(ScanParams P, RecordBuf R, Counters* C) {
+__global__ __launch_bounds__(SCAN_THREADS, 4) void k_face_scan(ScanParams P, RecordBuf R, Counters* C) {
     __shared__ Table T;
+    __shared__ uint4 stage_all[SCAN_THREADS / WAVE][WAVE];
+    constexpr bool STATS = MODE != MODE_GRAPH;
+    constexpr bool BND = MODE == MODE_BOUNDARY;
+    constexpr bool AFF = MODE == MODE_AFFINITY;
     const int tid = threadIdx.x;
     const int lane = tid & (WAVE - 1);
-    const int wave = tid >> 6;
+    // wave index through readfirstlane: row/plane coordinates become scalar
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    uint4* stage = stage_all[wave];
     for (int e = tid; e < TABLE_CAP; e += SCAN_THREADS) entry_reset(T, e);
     if (tid == 0) {
         T.used = 0;
@@ -207,122 +306,168 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_face_scan(ScanParams P, Record
 
     const int64_t Z = P.shape[0], Y = P.shape[1], X = P.shape[2];
     const int64_t sz = Y * X;
-    const int64_t x = (int64_t)blockIdx.x * TILE_X + lane;
-    const int64_t y0 = (int64_t)blockIdx.y * TILE_Y;
+    const int64_t x0 = (int64_t)blockIdx.x * TILE_X;
+    const int64_t x = x0 + lane;
+    const int64_t yw = (int64_t)blockIdx.y * WG_ROWS + wave * ROWS;   // first row of this wave
     const int64_t z0 = (int64_t)blockIdx.z * P.tile_z;
+    const int64_t z1 = min(z0 + (int64_t)P.tile_z, Z);
     const bool inx = x < X;
+    const bool hx = x + 1 < X;
     const LabelT* L = (const LabelT*)P.labels;
     const DataT* D = (const DataT*)P.data;
     const double scale = P.scale, offset = P.offset;
+    const bool fast40 = P.fast40 != 0;
     const int64_t obz = P.own_begin[0], oby = P.own_begin[1], obx = P.own_begin[2];
-    constexpr bool STATS = MODE != MODE_GRAPH;
-    constexpr bool BND = MODE == MODE_BOUNDARY;
-    const uint32_t adj_flag = (MODE == MODE_AFFINITY) ? ADJ_FLAG : 0u;
+    const int64_t oez = P.own_end[0], oey = P.own_end[1], oex = P.own_end[2];
+    const bool own_x_lo = x >= obx && x < oex;
+    const bool own_x_up = x + 1 >= obx && x + 1 < oex;
+    const int64_t xh = x0 + TILE_X;          // x of the lane-63 neighbour
+    const bool has_xh = xh < X;
 
-    // RAG face: key + (boundary) both voxel values as samples
-    auto face = [&](LabelT lp, LabelT lq, float dp, float dq, bool valid) {
-        if (!(valid && lp != lq)) return;
-        LabelT u = lp < lq ? lp : lq;
-        LabelT v = lp < lq ? lq : lp;
-        if constexpr (sizeof(LabelT) == 8) {
-            if (v >> 32) {
-                atomicAdd(&C->label_overflow, 1ull);
-                return;
+    // plane buffers: rows 0..ROWS-1 of this wave + the y-halo row; the x-halo
+    // voxel of row r lives in lane r of XL/XD
+    LabelT Lc[ROWS + 1], Ln[ROWS + 1];
+    float Dc[ROWS + 1], Dn[ROWS + 1];
+    LabelT XLc = 0, XLn = 0;
+    float XDc = 0.f, XDn = 0.f;
+
+    auto load_plane = [&](int64_t z, LabelT (&Lb)[ROWS + 1], float (&Db)[ROWS + 1], LabelT& XL, float& XD) {
+        const LabelT* Lz = L + z * sz + yw * X;
+        const DataT* Dz = BND ? D + z * sz + yw * X : nullptr;
+#pragma unroll
+        for (int r = 0; r <= ROWS; ++r) {
+            Lb[r] = 0;
+            Db[r] = 0.f;
+            if (inx && yw + r < Y) {
+                Lb[r] = Lz[r * X + x];
+                if constexpr (BND) Db[r] = load_val<DataT>(Dz, r * X + x);
             }
         }
-        const uint64_t key = ((uint64_t)u << 32) | (uint64_t)v;
-        const int s = table_insert(T, key);
-        if (s < 0) {
-            emit_direct(R, C, key, BND ? 2 : 0, dp, dq, scale, offset, adj_flag, STATS);
-            return;
+        XL = 0;
+        XD = 0.f;
+        if (lane < ROWS && has_xh && yw + lane < Y) {
+            XL = Lz[lane * X + xh];
+            if constexpr (BND) XD = load_val<DataT>(Dz, lane * X + xh);
         }
-        if constexpr (BND) add_samples<MODE>(T, s, 2, dp, dq, scale, offset);
-        if constexpr (MODE == MODE_AFFINITY) atomicOr(&T.w[s][21], ADJ_FLAG);
     };
 
-    for (int zs = 0; zs < P.tile_z; zs += 4) {
-        const int dz = zs + wave;
-        const int64_t z = z0 + dz;
-        if (dz < P.tile_z && z < Z) {
-            const bool hz = z + 1 < Z;
-            const bool own_z_lo = z >= obz;          // p_z >= own (faces along y, x)
-            const bool own_z_up = z + 1 >= obz;      // q_z >= own (face along z)
-            const bool own_x_lo = x >= obx;
-            const bool own_x_up = x + 1 >= obx;
-            int64_t i = z * sz + y0 * X + x;
-            LabelT cl = 0;
-            float cd = 0.f;
-            if (inx && y0 < Y) {
-                cl = L[i];
-                if constexpr (BND) cd = load_val<DataT>(D, i);
-            }
-            for (int dy = 0; dy < TILE_Y; ++dy) {
-                const int64_t y = y0 + dy;
-                if (y >= Y) break;
-                const bool hy = y + 1 < Y;
-                LabelT yl = 0, zl = 0, xl;
-                float yd = 0.f, zd = 0.f, xd;
-                if (inx) {
-                    if (hy) {
-                        yl = L[i + X];
-                        if constexpr (BND) yd = load_val<DataT>(D, i + X);
-                    }
-                    if (hz) {
-                        zl = L[i + sz];
-                        if constexpr (BND) zd = load_val<DataT>(D, i + sz);
-                    }
+    const int ablate = P.ablate;
+    uint64_t chk = 0;
+    bool ovf = false;
+    int nbuf = 0;   // staged faces (wave-uniform)
+
+    auto flush_stage = [&]() {
+        if (nbuf) {
+            fold_batch<MODE>(T, stage, nbuf, lane, R, C, fast40, scale, offset);
+            nbuf = 0;
+        }
+    };
+    // append the active lanes of one site to the stage
+    auto push = [&](bool act, uint64_t key, float a, uint32_t bbits) {
+        const uint64_t m = __ballot(act);
+        if (m == 0) return;
+        const int k = __popcll(m);
+        if (nbuf + k > WAVE) flush_stage();
+        if (act) {
+            const int rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+            stage[nbuf + rank] = make_uint4((uint32_t)key, (uint32_t)(key >> 32), __float_as_uint(a), bbits);
+        }
+        nbuf += k;
+    };
+    auto face_bits = [&](float b) -> uint32_t { return AFF ? MARK_ADJ : __float_as_uint(b); };
+
+    if (z0 < z1) load_plane(z0, Lc, Dc, XLc, XDc);
+    for (int64_t z = z0; z < z1; ++z) {
+        const bool hz = z + 1 < Z;
+        if (hz) load_plane(z + 1, Ln, Dn, XLn, XDn);        // prefetch: in flight during x/y faces
+        const bool own_z_lo = z >= obz && z < oez;
+        const bool own_z_up = z + 1 >= obz && z + 1 < oez;
+        if (ablate & 8) {   // diagnostic: loads only
+#pragma unroll
+            for (int r = 0; r < ROWS; ++r)
+                chk ^= (uint64_t)(Lc[r] ^ Lc[r + 1] ^ Ln[r]) + (uint64_t)__float_as_uint(Dc[r] + Dn[r]);
+        } else {
+#pragma unroll
+            for (int r = 0; r < ROWS; ++r) {
+                const int64_t y = yw + r;
+                const bool own_y_lo = y >= oby && y < oey;
+                const bool own_y_up = y + 1 >= oby && y + 1 < oey;
+                const LabelT lc = Lc[r];
+                // x face (x, x+1): lane 63 takes its neighbour from the x-halo
+                LabelT lx = shfl_down1<LabelT>(lc);
+                float dx = __shfl_down(Dc[r], 1, WAVE);
+                const LabelT xl63 = shfl_lane<LabelT>(XLc, r);
+                const float xd63 = __shfl(XDc, r, WAVE);
+                if (lane == WAVE - 1) {
+                    lx = xl63;
+                    dx = xd63;
                 }
-                xl = shfl_down1<LabelT>(cl);
-                xd = __shfl_down(cd, 1, WAVE);
-                const bool hx = x + 1 < X;
-                if (lane == WAVE - 1 && hx) {
-                    xl = L[i + 1];
-                    if constexpr (BND) xd = load_val<DataT>(D, i + 1);
-                }
-                const bool own_y_lo = y >= oby;
-                const bool own_y_up = y + 1 >= oby;
-                if (inx) {
-                    face(cl, xl, cd, xd, hx && own_z_lo && own_y_lo && own_x_up);
-                    face(cl, yl, cd, yd, hy && own_z_lo && own_y_up && own_x_lo);
-                    face(cl, zl, cd, zd, hz && own_z_up && own_y_lo && own_x_lo);
-                    if constexpr (MODE == MODE_AFFINITY) {
-                        // samples aff[c, p] for q = p + o_c, p in the owned box
-                        if (own_z_lo && own_y_lo && own_x_lo) {
-                            for (int c = 0; c < P.n_channels; ++c) {
-                                const int64_t qz = z + P.offsets[c][0];
-                                const int64_t qy = y + P.offsets[c][1];
-                                const int64_t qx = x + P.offsets[c][2];
-                                if (qz < 0 || qz >= Z || qy < 0 || qy >= Y || qx < 0 || qx >= X) continue;
-                                const LabelT lq = L[qz * sz + qy * X + qx];
-                                if (lq == cl) continue;
-                                LabelT u = cl < lq ? cl : lq;
-                                LabelT v = cl < lq ? lq : cl;
-                                if constexpr (sizeof(LabelT) == 8) {
-                                    if (v >> 32) {
-                                        atomicAdd(&C->label_overflow, 1ull);
-                                        continue;
-                                    }
-                                }
-                                const float a = load_val<DataT>(D, (int64_t)c * Z * sz + i);
-                                const uint64_t key = ((uint64_t)u << 32) | (uint64_t)v;
-                                const int s = table_insert(T, key);
-                                if (s < 0) {
-                                    emit_direct(R, C, key, 1, a, 0.f, scale, offset, 0u, true);
-                                    continue;
-                                }
-                                add_samples<MODE>(T, s, 1, a, 0.f, scale, offset);
-                            }
+                uint64_t key = 0;
+                bool act = y < Y && inx && hx && own_z_lo && own_y_lo && own_x_up && lc != lx;
+                if (act) act = make_key<LabelT>(lc, lx, key, ovf);
+                push(act, key, Dc[r], face_bits(dx));
+                // y face (y, y+1)
+                act = y + 1 < Y && inx && own_z_lo && own_y_up && own_x_lo && lc != Lc[r + 1];
+                if (act) act = make_key<LabelT>(lc, Lc[r + 1], key, ovf);
+                push(act, key, Dc[r], face_bits(Dc[r + 1]));
+                // affinity samples aff[c, p] for q = p + o_c, p in the owned box
+                if constexpr (AFF) {
+                    const bool own_p = y < Y && inx && own_z_lo && own_y_lo && own_x_lo;
+                    const int64_t i = z * sz + y * X + x;
+                    for (int c = 0; c < P.n_channels; ++c) {
+                        const int64_t qz = z + P.offsets[c][0];
+                        const int64_t qy = y + P.offsets[c][1];
+                        const int64_t qx = x + P.offsets[c][2];
+                        const bool inq = own_p && qz >= 0 && qz < Z && qy >= 0 && qy < Y && qx >= 0 && qx < X;
+                        LabelT lq = lc;
+                        float av = 0.f;
+                        if (inq) {
+                            lq = L[qz * sz + qy * X + qx];
+                            av = load_val<DataT>(D, (int64_t)c * Z * sz + i);
                         }
+                        bool sact = inq && lq != lc;
+                        if (sact) sact = make_key<LabelT>(lc, lq, key, ovf);
+                        push(sact, key, av, MARK_ONE);
                     }
                 }
-                cl = yl;
-                cd = yd;
-                i += X;
+            }
+            // z faces: plane z against the prefetched plane z+1
+            if (hz) {
+#pragma unroll
+                for (int r = 0; r < ROWS; ++r) {
+                    const int64_t y = yw + r;
+                    const bool own_y_lo = y >= oby && y < oey;
+                    uint64_t key = 0;
+                    bool act = y < Y && inx && own_z_up && own_y_lo && own_x_lo && Lc[r] != Ln[r];
+                    if (act) act = make_key<LabelT>(Lc[r], Ln[r], key, ovf);
+                    push(act, key, Dc[r], face_bits(Dn[r]));
+                }
             }
         }
-        __syncthreads();
-        if (T.used > TABLE_CAP / 2) table_flush<MODE>(T, R, C);
+        // plane done: fold the staged faces (exact counts for the u16 guard),
+        // then decide on a flush
+        flush_stage();
+        if (!(ablate & 16)) {
+            __syncthreads();
+            bool need = tid == 0 && T.used > TABLE_CAP / 2;
+            if constexpr (STATS) {
+                for (int e = tid; e < TABLE_CAP; e += SCAN_THREADS) need |= (T.w[e][21] & ~ADJ_FLAG) > P.hist_guard;
+            }
+            if (__syncthreads_or(need)) table_flush<MODE>(T, R, C);
+        }
+#pragma unroll
+        for (int r = 0; r <= ROWS; ++r) {
+            Lc[r] = Ln[r];
+            Dc[r] = Dn[r];
+        }
+        XLc = XLn;
+        XDc = XDn;
     }
+    if (ablate & 8) {
+        if (chk == 0x9E3779B97F4A7C15ull) atomicAdd(&C->pad[0], 1ull);
+    }
+    if (__ballot(ovf) && lane == 0) atomicAdd(&C->label_overflow, 1ull);
+    flush_stage();
     table_flush<MODE>(T, R, C);
 }
 
@@ -331,7 +476,7 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_face_scan(ScanParams P, Record
 // ---------------------------------------------------------------------------
 template <typename LabelT, typename DataT, int MODE>
 static hipError_t launch_scan_t(const ScanParams& P, const RecordBuf& R, Counters* C, hipStream_t s) {
-    dim3 grid((unsigned)((P.shape[2] + TILE_X - 1) / TILE_X), (unsigned)((P.shape[1] + TILE_Y - 1) / TILE_Y),
+    dim3 grid((unsigned)((P.shape[2] + TILE_X - 1) / TILE_X), (unsigned)((P.shape[1] + WG_ROWS - 1) / WG_ROWS),
               (unsigned)((P.shape[0] + P.tile_z - 1) / P.tile_z));
     hipLaunchKernelGGL((k_face_scan<LabelT, DataT, MODE>), grid, dim3(SCAN_THREADS), 0, s, P, R, C);
     return hipGetLastError();
@@ -357,20 +502,20 @@ hipError_t launch_face_scan(const ScanParams& P, const RecordBuf& R, Counters* C
 // ---------------------------------------------------------------------------
 // unique labels of a box (per-block ``nodes``): LDS hash set per tile
 // ---------------------------------------------------------------------------
+constexpr int UNIQ_THREADS = 256;  // 4 waves: the unique-label scan walks 4 planes per step
 constexpr int USET_CAP = 2048;
 
-__global__ __launch_bounds__(SCAN_THREADS) void k_unique_tiles(const uint64_t* L, int64_t Y, int64_t X,
+__global__ __launch_bounds__(UNIQ_THREADS) void k_unique_tiles(const uint64_t* L, int64_t Y, int64_t X,
                                                                 int64_t bz, int64_t by, int64_t bx,
                                                                 int64_t ez, int64_t ey, int64_t ex,
                                                                 uint64_t* out, unsigned long long* count,
                                                                 int64_t cap) {
     __shared__ uint64_t set[USET_CAP];
     __shared__ uint32_t used;
-    __shared__ uint32_t n;
     __shared__ unsigned long long base;
-    __shared__ uint32_t w;
+    __shared__ uint32_t wpos;
     const int tid = threadIdx.x;
-    for (int e = tid; e < USET_CAP; e += SCAN_THREADS) set[e] = EMPTY_KEY;
+    for (int e = tid; e < USET_CAP; e += UNIQ_THREADS) set[e] = EMPTY_KEY;
     if (tid == 0) used = 0;
     __syncthreads();
     const int lane = tid & 63, wave = tid >> 6;
@@ -396,7 +541,10 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_unique_tiles(const uint64_t* L
                         if (cur == EMPTY_KEY) {
                             uint64_t old = atomicCAS((unsigned long long*)&set[h], (unsigned long long)EMPTY_KEY,
                                                      (unsigned long long)l);
-                            if (old == EMPTY_KEY) { atomicAdd(&used, 1u); break; }
+                            if (old == EMPTY_KEY) {
+                                atomicAdd(&used, 1u);
+                                break;
+                            }
                             if (old == l) break;
                         }
                         h = (h + 1) & (USET_CAP - 1);
@@ -407,17 +555,15 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_unique_tiles(const uint64_t* L
         __syncthreads();
         if (used > USET_CAP / 2 || zs + 4 >= 16) {
             if (tid == 0) {
-                n = used;
                 base = atomicAdd(count, (unsigned long long)used);
+                wpos = 0;
             }
             __syncthreads();
             // compaction order is irrelevant (sorted afterwards)
-            if (tid == 0) w = 0;
-            __syncthreads();
-            for (int e = tid; e < USET_CAP; e += SCAN_THREADS) {
+            for (int e = tid; e < USET_CAP; e += UNIQ_THREADS) {
                 uint64_t k = set[e];
                 if (k != EMPTY_KEY) {
-                    uint32_t r = atomicAdd(&w, 1u);
+                    uint32_t r = atomicAdd(&wpos, 1u);
                     if (base + r < (unsigned long long)cap) out[base + r] = k;
                     set[e] = EMPTY_KEY;
                 }
@@ -433,7 +579,7 @@ hipError_t launch_unique_tiles(const uint64_t* L, const int64_t* shape, const in
                                uint64_t* out, unsigned long long* count, int64_t cap, hipStream_t s) {
     dim3 grid((unsigned)((e[2] - b[2] + 63) / 64), (unsigned)((e[1] - b[1] + TILE_Y - 1) / TILE_Y),
               (unsigned)((e[0] - b[0] + 15) / 16));
-    hipLaunchKernelGGL(k_unique_tiles, grid, dim3(SCAN_THREADS), 0, s, L, shape[1], shape[2], b[0], b[1], b[2],
+    hipLaunchKernelGGL(k_unique_tiles, grid, dim3(UNIQ_THREADS), 0, s, L, shape[1], shape[2], b[0], b[1], b[2],
                        e[0], e[1], e[2], out, count, cap);
     return hipGetLastError();
 }

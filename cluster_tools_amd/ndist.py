@@ -1,0 +1,360 @@
+"""Drop-in mirror of the ``nifty.distributed`` functions on the hot path.
+
+The reference's job bodies do ``import nifty.distributed as ndist`` and call
+the functions below with container paths, keys and block ids; each call does
+its own N5 I/O and returns None.  This module keeps the names,
+argument order/keywords and on-disk effects, and runs the array work through
+libctg.so (``cluster_tools_amd.rag``) on the GPU.  Swapping the import is the
+whole integration:
+
+    computeMergeableRegionGraph    graph/initial_sub_graphs.py:124-129
+    mergeSubgraphs                 graph/merge_sub_graphs.py:130-135, 147-150
+    mapEdgeIds                     graph/map_edge_ids.py:116-119
+    extractBlockFeaturesFromBoundaryMaps_{float32,uint8}
+                                   features/block_edge_features.py:127-134
+    extractBlockFeaturesFromAffinityMaps_{float32,uint8}
+                                   features/block_edge_features.py:138-145
+    mergeFeatureBlocks             features/merge_edge_features.py:141-147
+    Graph                          test/graph/test_graph.py:32,68,111;
+                                   multicut/solve_subproblems.py:250
+
+Errors surface as RuntimeError (``_lib.CtgError``), as pybind11 raises for
+nifty's C++ exceptions, so a failing job never prints ``processed job N`` and
+the reference's retry logic (cluster_tasks.py:114-159) applies unchanged.
+"""
+from __future__ import annotations
+
+import os
+from concurrent.futures import ThreadPoolExecutor
+
+import numpy as np
+
+from . import n5
+from . import rag
+from .blocking import blocking
+
+N_FEATURES = 10
+STATS_SUFFIX = '_stats'   # companion varlen dataset: per edge (sum, sumsq, 48 record words)
+STATS_WIDTH = 2 + rag.WIDE_WORDS
+
+
+def _open(path, mode='a'):
+    return n5.File(path, mode)
+
+
+def _map(fn, items, n_threads):
+    items = list(items)
+    if n_threads and n_threads > 1 and len(items) > 1:
+        with ThreadPoolExecutor(int(n_threads)) as ex:
+            return list(ex.map(fn, items))
+    return [fn(i) for i in items]
+
+
+def _roi(ds, begin, end):
+    return ds[tuple(slice(int(b), int(e)) for b, e in zip(begin, end))]
+
+
+def _subgraph_blocking(g):
+    shape = [int(s) for s in g.attrs.get('shape', g['nodes'].shape)]
+    return blocking([0, 0, 0], shape, list(g['nodes'].chunks)), shape
+
+
+# ---------------------------------------------------------------------------
+# graph
+# ---------------------------------------------------------------------------
+
+def computeMergeableRegionGraph(labelsPath, labelsKey, roiBegin, roiEnd, graphPath,  # noqa: N802,N803
+                                subgraphKey, ignoreLabel, increaseRoi=True, serializeToVarlen=True):  # noqa: N803
+    """Per-block sub-graph: sorted unique labels of the inner block (varlen
+    ``nodes`` chunk) and the sorted unique (u<v) RAG edges of
+    labels[max(begin-1,0):end] (varlen ``edges`` chunk, flattened; no chunk if
+    empty), semantics of test/graph/test_graph.py:42-84."""
+    if not serializeToVarlen:
+        raise NotImplementedError('computeMergeableRegionGraph only serializes to varlen chunks '
+                                  '(the only mode the reference uses, initial_sub_graphs.py:129)')
+    roiBegin = [int(b) for b in roiBegin]
+    roiEnd = [int(e) for e in roiEnd]
+    begin = [max(b - 1, 0) for b in roiBegin] if increaseRoi else list(roiBegin)
+    with _open(labelsPath, 'r') as f:
+        labels = _roi(f[labelsKey], begin, roiEnd)
+    labels = np.ascontiguousarray(labels.astype(np.uint64, copy=False))
+    inner_b = [b - o for b, o in zip(roiBegin, begin)]
+    inner_e = [e - o for e, o in zip(roiEnd, begin)]
+    nodes = rag.unique_labels(labels, inner_b, inner_e)
+    edges = rag.rag_features(labels, None, ignore_label=bool(ignoreLabel))['edges']
+    with _open(graphPath) as f:
+        g = f[subgraphKey]
+        ds_nodes = g['nodes']
+        pos = [b // c for b, c in zip(roiBegin, ds_nodes.chunks)]
+        ds_nodes.write_chunk(pos, nodes, True)
+        if edges.shape[0]:
+            g['edges'].write_chunk(pos, edges.ravel(), True)
+
+
+def _read_block_graph(g, pos):
+    nodes = g['nodes'].read_chunk(pos)
+    edges = g['edges'].read_chunk(pos)
+    edges = None if edges is None else edges.reshape(-1, 2)
+    return nodes, edges
+
+
+def mergeSubgraphs(graphPath, subgraphKey, blockIds, outKey, numberOfThreads=1,  # noqa: N802,N803
+                   serializeToVarlen=False):  # noqa: N803
+    """Union of block sub-graphs.  serializeToVarlen=False writes the merged
+    graph ``outKey/{nodes,edges}`` with attrs numberOfNodes / numberOfEdges
+    (merge_sub_graphs.py:127-137); True writes one varlen chunk of the next
+    scale's sub-graph dataset (merge_sub_graphs.py:140-152)."""
+    with _open(graphPath) as f:
+        g = f[subgraphKey]
+        blk, shape = _subgraph_blocking(g)
+        block_ids = [int(b) for b in blockIds]
+        parts = _map(lambda b: _read_block_graph(g, blk.blockGridPosition(b)), block_ids, numberOfThreads)
+        node_list = [p[0] for p in parts if p[0] is not None and len(p[0])]
+        edge_list = [p[1] for p in parts if p[1] is not None and len(p[1])]
+        nodes = np.concatenate(node_list).astype(np.uint64) if node_list else np.zeros(0, np.uint64)
+        if nodes.size:
+            nodes = rag.unique_labels(nodes.reshape(1, 1, -1))
+        if edge_list:
+            edges, _ = rag.unique_pairs(np.concatenate(edge_list, axis=0))
+        else:
+            edges = np.zeros((0, 2), np.uint64)
+        if serializeToVarlen:
+            out = f[outKey]
+            out_chunks = out['nodes'].chunks
+            first = blk.getBlock(block_ids[0]) if block_ids else None
+            if first is None:
+                return
+            pos = [b // c for b, c in zip(first.begin, out_chunks)]
+            out['nodes'].write_chunk(pos, nodes, True)
+            if edges.shape[0]:
+                out['edges'].write_chunk(pos, edges.ravel(), True)
+            return
+        out = f.require_group(outKey)
+        n_nodes, n_edges = int(nodes.shape[0]), int(edges.shape[0])
+        ds_n = out.require_dataset('nodes', shape=(n_nodes,), chunks=(max(1, min(n_nodes, 262144)),),
+                                   dtype='uint64', compression='gzip')
+        ds_e = out.require_dataset('edges', shape=(n_edges, 2), chunks=(max(1, min(n_edges, 262144)), 2),
+                                   dtype='uint64', compression='gzip')
+        ds_n.n_threads = ds_e.n_threads = max(1, int(numberOfThreads))
+        if n_nodes:
+            ds_n[:] = nodes
+        if n_edges:
+            ds_e[:] = edges
+        out.attrs['numberOfNodes'] = n_nodes
+        out.attrs['numberOfEdges'] = n_edges
+
+
+def mapEdgeIds(graphPath, graphKey, subgraphKey, blockIds, numberOfThreads=1):  # noqa: N802,N803
+    """Per block: global edge id of every local edge (varlen uint64
+    ``edge_ids`` chunk), = full_graph.findEdges(uv) (test_graph.py:89-93)."""
+    with _open(graphPath) as f:
+        global_edges = f[graphKey]['edges'][:]
+        g = f[subgraphKey]
+        blk, _ = _subgraph_blocking(g)
+        block_ids = [int(b) for b in blockIds]
+        chunks = _map(lambda b: g['edges'].read_chunk(blk.blockGridPosition(b)), block_ids, numberOfThreads)
+        have = [(b, c.reshape(-1, 2)) for b, c in zip(block_ids, chunks) if c is not None and c.size]
+        if not have:
+            return
+        query = np.concatenate([c for _, c in have], axis=0)
+        ids = rag.map_edge_ids(global_edges, query)
+        if (ids < 0).any():
+            raise RuntimeError('mapEdgeIds: %d sub-graph edges are missing from the merged graph'
+                               % int((ids < 0).sum()))
+        ds = g['edge_ids']
+        off = 0
+        writes = []
+        for b, c in have:
+            writes.append((blk.blockGridPosition(b), ids[off:off + c.shape[0]].astype(np.uint64)))
+            off += c.shape[0]
+        _map(lambda w: ds.write_chunk(w[0], w[1], True), writes, numberOfThreads)
+
+
+class Graph:
+    """ndist.Graph: a graph over arbitrary uint64 node ids.
+
+    Graph(edges) | Graph(path, key, numberOfThreads=n).  numberOfNodes is the
+    count of distinct nodes (test_graph.py:80-81, reduce_problem.py:322-326).
+    """
+
+    def __init__(self, *args, numberOfThreads=1):  # noqa: N803
+        nodes = None
+        if len(args) == 1 and not isinstance(args[0], str):
+            edges = np.asarray(args[0], dtype=np.uint64).reshape(-1, 2)
+        elif len(args) >= 2:
+            with _open(args[0], 'r') as f:
+                g = f[args[1]]
+                edges = g['edges'][:] if 'edges' in g else np.zeros((0, 2), np.uint64)
+                if 'nodes' in g:
+                    nodes = g['nodes'][:]
+        else:
+            raise TypeError('Graph(edges) or Graph(path, key)')
+        self._uv = np.ascontiguousarray(edges.reshape(-1, 2).astype(np.uint64))
+        self._nodes = np.unique(self._uv) if nodes is None else np.asarray(nodes, dtype=np.uint64)
+        self._sorted = None
+
+    @property
+    def numberOfNodes(self):  # noqa: N802
+        return int(self._nodes.shape[0])
+
+    @property
+    def numberOfEdges(self):  # noqa: N802
+        return int(self._uv.shape[0])
+
+    @property
+    def maxNodeId(self):  # noqa: N802
+        return int(self._nodes.max()) if self._nodes.size else 0
+
+    @property
+    def maxEdgeId(self):  # noqa: N802
+        return self.numberOfEdges - 1
+
+    def uvIds(self):  # noqa: N802
+        return self._uv
+
+    def nodes(self):
+        return self._nodes
+
+    def findEdges(self, uv):  # noqa: N802
+        uv = np.asarray(uv, dtype=np.uint64).reshape(-1, 2)
+        if self._sorted is None:
+            order = np.lexsort((self._uv[:, 1], self._uv[:, 0]))
+            self._sorted = (order, np.ascontiguousarray(self._uv[order]))
+        order, srt = self._sorted
+        pos = rag.map_edge_ids(srt, uv)
+        return np.where(pos >= 0, order[np.maximum(pos, 0)], -1).astype(np.int64)
+
+    def findEdge(self, u, v):  # noqa: N802
+        return int(self.findEdges(np.array([[u, v]], dtype=np.uint64))[0])
+
+
+# ---------------------------------------------------------------------------
+# features
+# ---------------------------------------------------------------------------
+
+def _write_block_features(fo, outKey, pos, shape, chunks, feats, sums, records):  # noqa: N803
+    ds = fo[outKey]
+    ds.write_chunk(pos, feats.ravel(), True)
+    st = fo.require_dataset(outKey + STATS_SUFFIX, shape=shape, chunks=chunks, dtype='float64',
+                            compression='gzip')
+    stats = np.zeros((feats.shape[0], STATS_WIDTH), dtype=np.float64)
+    stats[:, :2] = sums
+    stats[:, 2:] = records.astype(np.float64)
+    st.write_chunk(pos, stats.ravel(), True)
+
+
+def _block_features(graphPath, subgraphKey, dataPath, dataKey, labelsPath, labelsKey, blockIds,  # noqa: N803
+                    outPath, outKey, halo_lo, halo_hi, offsets, increaseRoi):  # noqa: N803
+    with _open(graphPath, 'r') as fg:
+        g = fg[subgraphKey]
+        blk, shape = _subgraph_blocking(g)
+        ignore = bool(g.attrs.get('ignore_label', False))
+        ds_edges = g['edges']
+        chunks = g['nodes'].chunks
+        with _open(dataPath, 'r') as fd, _open(labelsPath, 'r') as fl, _open(outPath) as fo:
+            ds_data = fd[dataKey]
+            ds_lab = fl[labelsKey]
+            for bid in [int(b) for b in blockIds]:
+                block = blk.getBlock(bid)
+                pos = blk.blockGridPosition(bid)
+                edges_b = ds_edges.read_chunk(pos)
+                if edges_b is None:
+                    continue
+                edges_b = edges_b.reshape(-1, 2)
+                lo = halo_lo if increaseRoi else [0, 0, 0]
+                rb = [max(b - h, 0) for b, h in zip(block.begin, lo)]
+                re_ = [min(e + h, s) for e, h, s in zip(block.end, halo_hi, shape)]
+                labels = np.ascontiguousarray(_roi(ds_lab, rb, re_).astype(np.uint64, copy=False))
+                if offsets is None:
+                    data = _roi(ds_data, rb, re_)
+                else:
+                    data = ds_data[(slice(0, len(offsets)),) + tuple(slice(b, e) for b, e in zip(rb, re_))]
+                own_b = [b - r for b, r in zip(block.begin, rb)]
+                own_e = [e - r for e, r in zip(block.end, rb)]
+                res = rag.rag_features(labels, data, offsets=offsets, own_begin=own_b, own_end=own_e,
+                                       ignore_label=ignore, keep_stats=True)
+                rows = rag.map_edge_ids(res['edges'], edges_b) if res['edges'].shape[0] else \
+                    np.full(edges_b.shape[0], -1, np.int64)
+                hit = rows >= 0
+                feats = np.zeros((edges_b.shape[0], N_FEATURES), np.float64)
+                sums = np.zeros((edges_b.shape[0], 2), np.float64)
+                recs = np.zeros((edges_b.shape[0], rag.WIDE_WORDS), np.uint32)
+                feats[hit] = res['features'][rows[hit]]
+                sums[hit] = res['sums'][rows[hit]]
+                recs[hit] = res['records'][rows[hit]]
+                _write_block_features(fo, outKey, pos, shape, chunks, feats, sums, recs)
+
+
+def extractBlockFeaturesFromBoundaryMaps_float32(graphPath, subgraphKey, dataPath, dataKey,  # noqa: N802,N803
+                                                 labelsPath, labelsKey, blockIds, outPath, outKey,  # noqa: N803
+                                                 increaseRoi=True):  # noqa: N803
+    """Per-block 10 edge features of the block's sub-graph edges from a float32
+    boundary map; every face counted once globally (owned by the block holding
+    its upper voxel), both voxel values are samples."""
+    _block_features(graphPath, subgraphKey, dataPath, dataKey, labelsPath, labelsKey, blockIds, outPath,
+                    outKey, [1, 1, 1], [0, 0, 0], None, increaseRoi)
+
+
+def extractBlockFeaturesFromBoundaryMaps_uint8(*args, **kw):  # noqa: N802
+    """uint8 boundary maps: samples are value/255 (SURVEY OPEN-7)."""
+    extractBlockFeaturesFromBoundaryMaps_float32(*args, **kw)
+
+
+def extractBlockFeaturesFromAffinityMaps_float32(graphPath, subgraphKey, dataPath, dataKey,  # noqa: N802,N803
+                                                 labelsPath, labelsKey, blockIds, outPath, outKey,  # noqa: N803
+                                                 offsets):
+    """Per-block features from channel-first affinities: sample aff[c,p] for
+    every p in the block with L[p] != L[p+o_c] and (min,max) an edge of the
+    block's sub-graph."""
+    off = np.asarray(offsets, dtype=np.int64).reshape(-1, 3)
+    halo_lo = [max(1, int(max(0, -off[:, a].min()))) for a in range(3)]
+    halo_hi = [int(max(0, off[:, a].max())) for a in range(3)]
+    _block_features(graphPath, subgraphKey, dataPath, dataKey, labelsPath, labelsKey, blockIds, outPath,
+                    outKey, halo_lo, halo_hi, off.tolist(), True)
+
+
+def extractBlockFeaturesFromAffinityMaps_uint8(*args, **kw):  # noqa: N802
+    extractBlockFeaturesFromAffinityMaps_float32(*args, **kw)
+
+
+def mergeFeatureBlocks(graphPath, subgraphKey, featuresPath, featuresKey, outPath, outKey,  # noqa: N802,N803
+                       blockIds, edgeIdBegin, edgeIdEnd, numberOfThreads=1):  # noqa: N803
+    """Combine the per-block feature rows of edges in [edgeIdBegin, edgeIdEnd)
+    into rows of the (E,10) ``outKey`` dataset: counts add, mean count-weighted,
+    variance by Chan's formula, min/max over non-empty blocks, quantiles from
+    the merged histograms (exact; SURVEY OPEN-3 default)."""
+    begin, end = int(edgeIdBegin), int(edgeIdEnd)
+    with _open(graphPath, 'r') as fg, _open(featuresPath, 'r') as ff:
+        g = fg[subgraphKey]
+        blk, _ = _subgraph_blocking(g)
+        ds_ids = g['edge_ids']
+        if featuresKey + STATS_SUFFIX not in ff:
+            raise RuntimeError('mergeFeatureBlocks: %s has no %s companion dataset; the block features were '
+                               'not written by cluster_tools_amd' % (featuresKey, STATS_SUFFIX))
+        ds_st = ff[featuresKey + STATS_SUFFIX]
+
+        def load(b):
+            pos = blk.blockGridPosition(int(b))
+            ids = ds_ids.read_chunk(pos)
+            if ids is None:
+                return None
+            st = ds_st.read_chunk(pos)
+            if st is None:
+                return None
+            st = st.reshape(-1, STATS_WIDTH)
+            sel = (ids >= begin) & (ids < end)
+            return ids[sel], st[sel]
+
+        parts = [p for p in _map(load, blockIds, numberOfThreads) if p is not None and len(p[0])]
+    out = np.zeros((end - begin, N_FEATURES), np.float64)
+    if parts:
+        ids = np.concatenate([p[0] for p in parts]).astype(np.uint64)
+        st = np.concatenate([p[1] for p in parts], axis=0)
+        keys = np.zeros((ids.shape[0], 2), np.uint64)
+        keys[:, 1] = ids
+        recs = st[:, 2:].astype(np.uint32)
+        recs[:, 42] |= np.uint32(0x80000000)   # every block row is a graph edge
+        merged = rag.merge_stats(keys, st[:, :2], recs)
+        out[merged['edges'][:, 1].astype(np.int64) - begin] = merged['features']
+    with _open(outPath) as fo:
+        fo[outKey][begin:end, :] = out

@@ -128,7 +128,7 @@ def _check_offsets(offsets):
     return off
 
 
-def rag_features_handle(labels, data=None, offsets=None, own_begin=None, ignore_label=False,
+def rag_features_handle(labels, data=None, offsets=None, own_begin=None, own_end=None, ignore_label=False,
                         hist_range=(0.0, 1.0), keep_stats=False, stream=None):
     """Run the hot path and return the device-resident ``Result`` handle.
 
@@ -184,10 +184,11 @@ def rag_features_handle(labels, data=None, offsets=None, own_begin=None, ignore_
             raise ValueError('boundary map shape %s != labels shape %s' % (tuple(data.shape), tuple(shape)))
     sh = _shape_arr(shape)
     ob = _shape_arr(own_begin) if own_begin is not None else None
+    oe = _shape_arr(own_end) if own_end is not None else None
     if stream is None:
         stream = _current_stream(on_dev)
     h = ctypes.c_void_p()
-    rc = lib.ctg_rag_features(_ptr(labels), label_bits, _ptr(data), kind, n_ch, off_ptr, sh, ob,
+    rc = lib.ctg_rag_features(_ptr(labels), label_bits, _ptr(data), kind, n_ch, off_ptr, sh, ob, oe,
                               int(bool(ignore_label)), float(hist_range[0]), float(hist_range[1]),
                               int(bool(keep_stats)), L.CTG_MEM_DEVICE if on_dev else L.CTG_MEM_HOST,
                               stream, ctypes.byref(h))
@@ -195,10 +196,10 @@ def rag_features_handle(labels, data=None, offsets=None, own_begin=None, ignore_
     return Result(h, dev)
 
 
-def rag_features(labels, data=None, offsets=None, own_begin=None, ignore_label=False,
+def rag_features(labels, data=None, offsets=None, own_begin=None, own_end=None, ignore_label=False,
                  hist_range=(0.0, 1.0), keep_stats=False):
     """Host convenience: returns dict(edges, nodes, features[, sums, records])."""
-    r = rag_features_handle(labels, data, offsets, own_begin, ignore_label, hist_range, keep_stats)
+    r = rag_features_handle(labels, data, offsets, own_begin, own_end, ignore_label, hist_range, keep_stats)
     out = dict(edges=r.edges(), nodes=r.nodes())
     if data is not None:
         out['features'] = r.features()
@@ -247,6 +248,19 @@ def merge_stats(keys, sums, records, hist_range=(0.0, 1.0), keep_stats=False):
     out = dict(edges=r.edges(), features=r.features())
     if keep_stats:
         out['sums'], out['records'] = r.stats()
+    r.free()
+    return out
+
+
+def unique_pairs(pairs):
+    """Sorted unique rows of an (n,2) uint64 pair list -> (edges, nodes)."""
+    lib = L.load()
+    dev = L.init_device()
+    p = np.ascontiguousarray(np.asarray(pairs, dtype=np.uint64).reshape(-1, 2))
+    h = ctypes.c_void_p()
+    L.check(lib.ctg_unique_pairs(_ptr(p), p.shape[0], L.CTG_MEM_HOST, None, ctypes.byref(h)), 'ctg_unique_pairs')
+    r = Result(h, dev)
+    out = r.edges(), r.nodes()
     r.free()
     return out
 

@@ -53,7 +53,7 @@ extern "C" {
 #define CTG_DATA_F32 1
 #define CTG_DATA_U8 2     /* mapped to [0,1] by /255 before binning (SURVEY OPEN-7) */
 
-#define CTG_MAX_CHANNELS 32
+#define CTG_MAX_CHANNELS 24
 #define CTG_N_FEATURES 10
 #define CTG_NBINS 40
 #define CTG_WIDE_RECORD_WORDS 48  /* u32 words of one wide statistics record */
@@ -71,10 +71,10 @@ int ctg_device_count(int* count);
  *   labels     uint64 (label_bits=64) or uint32 (label_bits=32), C-order (Z,Y,X)
  *   data       NULL, boundary map (Z,Y,X) or channel-first affinities (C,Z,Y,X)
  *   offsets    NULL for a boundary map, else n_channels x 3 int32 (z,y,x) offsets
- *   own_begin  faces / samples are counted only when their owning voxel lies in
- *              [own_begin, shape): the upper voxel of a face, the voxel p of an
- *              affinity sample.  NULL = whole array.  A 1-voxel own_begin is the
- *              lower-halo geometry of increaseRoi=True.
+ *   own_begin, own_end  faces / samples are counted only when their owning
+ *              voxel lies in [own_begin, own_end): the upper voxel of a face, the
+ *              voxel p of an affinity sample.  NULL = 0 / shape.  A 1-voxel
+ *              own_begin is the lower-halo geometry of increaseRoi=True.
  *   ignore_label  drop edges that contain label 0 (nodes still contain 0)
  *   hist_lo/hi    histogram range (nifty: [0,1])
  * Result: sorted unique edges (u<v, lexicographic), sorted unique nodes and,
@@ -84,7 +84,7 @@ int ctg_device_count(int* count);
 int ctg_rag_features(const void* labels, int label_bits,
                      const void* data, int data_kind,
                      int n_channels, const int32_t* offsets,
-                     const int64_t* shape, const int64_t* own_begin,
+                     const int64_t* shape, const int64_t* own_begin, const int64_t* own_end,
                      int ignore_label, double hist_lo, double hist_hi,
                      int keep_stats, int mem, void* stream, ctg_result** out);
 
@@ -100,6 +100,10 @@ int ctg_unique_labels(const uint64_t* labels, const int64_t* shape,
 int ctg_merge_stats(const uint64_t* keys, const double* sums, const uint32_t* records,
                     int64_t n, double hist_lo, double hist_hi, int keep_stats,
                     int mem, void* stream, ctg_result** out);
+
+/* sorted unique (u,v) pairs of an (n,2) uint64 list (union of block sub-graph
+ * edge lists, ndist.mergeSubgraphs); result nodes = unique endpoints */
+int ctg_unique_pairs(const uint64_t* pairs, int64_t n, int mem, void* stream, ctg_result** out);
 
 /* position of each query (u,v) in the sorted global edge table, -1 if absent */
 int ctg_map_edge_ids(const uint64_t* global_edges, int64_t n_global,
