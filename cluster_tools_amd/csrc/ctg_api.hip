@@ -458,7 +458,11 @@ int ctg_rag_features(const void* labels, int label_bits, const void* data, int d
     // the 64x32 tile cross-section; the scan flushes its LDS table before any
     // entry could reach 65535 within the next plane.
     const int spv = P.n_channels > 0 ? std::max(P.n_channels, 3) : 6;
-    P.hist_guard = (uint32_t)(65535 - spv * TILE_X * 32);
+    // (plus 2 samples for each of the 64 staged faces of each of the 8 waves)
+    // (checked every 4 planes, plus 2 samples for each of the 64 staged faces
+    // of each of the 8 waves)
+    P.check_planes = std::max(1, std::min(4, (65535 - 2 * 64 * 8) / (spv * TILE_X * 32)));
+    P.hist_guard = (uint32_t)(65535 - P.check_planes * spv * TILE_X * 32 - 2 * 64 * 8);
     // planes per workgroup: deep tiles (fewer records), but >= ~1024 workgroups
     {
         const int64_t cols = ((shape[2] + TILE_X - 1) / TILE_X) * ((shape[1] + 31) / 32);
@@ -506,6 +510,9 @@ int ctg_rag_features(const void* labels, int label_bits, const void* data, int d
     const int64_t n = (int64_t)w.counters_host->n_records;
     w.last_records = n;
     w.last_direct = (int64_t)w.counters_host->n_direct;
+    if (P.ablate & 256)
+        fprintf(stderr, "ctg stamps (wave-cycles): total %llu fold %llu flush %llu check-barrier %llu\n",
+                w.counters_host->pad[0], w.counters_host->pad[2], w.counters_host->pad[3], w.counters_host->pad[1]);
 
     ctg_result* r = new ctg_result();
     r->device = dev;

@@ -29,8 +29,11 @@ struct __align__(16) Table {
     uint64_t key[TABLE_CAP];
     double sum[TABLE_CAP];
     double sq[TABLE_CAP];
-    uint32_t w[TABLE_CAP][NREC_WORDS];   // hist words 0..20, 21 cnt|ADJ, 22 min, 23 max
+    // hist words 0..20, 21 cnt|ADJ, 22 min, 23 max; odd row stride (25 words)
+    // so atomics to different entries spread over the 32 LDS banks
+    uint32_t w[TABLE_CAP][NREC_WORDS + 1];
     uint16_t compact[TABLE_CAP];
+    uint32_t wave_cnt[SCAN_THREADS / WAVE];
     uint32_t used;
     uint32_t ncompact;
     unsigned long long base;
@@ -48,7 +51,8 @@ __device__ __forceinline__ void entry_reset(Table& T, int e) {
 }
 
 // home bucket of a key: two slots (even, odd) read by one ds_read_b128
-__device__ __forceinline__ uint32_t home_bucket(uint64_t key) { return hash_key(key) & (TABLE_CAP - 2); }
+// home bucket of a key: four slots, read by two ds_read_b128
+__device__ __forceinline__ uint32_t home_bucket(uint64_t key) { return hash_key(key) & (TABLE_CAP - 4); }
 
 // linear probing from the home bucket; returns the slot or -1 when full
 __device__ __forceinline__ int table_insert(Table& T, uint64_t key) {
@@ -73,20 +77,35 @@ __device__ __forceinline__ int table_insert(Table& T, uint64_t key) {
 
 template <int MODE>
 __device__ void table_flush(Table& T, RecordBuf R, Counters* C) {
+    static_assert(TABLE_CAP == SCAN_THREADS, "one table entry per thread in the flush");
     __syncthreads();
     const int tid = threadIdx.x;
-    uint64_t mv = 0;
-    for (int e = tid; e < TABLE_CAP; e += SCAN_THREADS) {
-        uint64_t k = T.key[e];
-        if (k != EMPTY_KEY) {
-            uint32_t r = atomicAdd(&T.ncompact, 1u);
-            T.compact[r] = (uint16_t)e;
-            mv = max(mv, k & 0xFFFFFFFFull);
-        }
+    const int lane = tid & (WAVE - 1), wv = tid >> 6;
+    // ballot compaction: entry tid goes to wave offset + rank among its wave
+    const uint64_t k = T.key[tid];
+    const bool live = k != EMPTY_KEY;
+    const uint64_t m = __ballot(live);
+    const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+    uint64_t mv = live ? (k & 0xFFFFFFFFull) : 0ull;
+    for (int o = 32; o > 0; o >>= 1) {
+        const uint64_t other = ((uint64_t)__shfl_xor((uint32_t)(mv >> 32), o, WAVE) << 32) |
+                               __shfl_xor((uint32_t)mv, o, WAVE);
+        mv = max(mv, other);
     }
-    if (mv) atomicMax(&T.maxv, (unsigned long long)mv);
+    if (lane == 0) {
+        T.wave_cnt[wv] = (uint32_t)__popcll(m);
+        if (mv) atomicMax(&T.maxv, (unsigned long long)mv);
+    }
     __syncthreads();
-    const uint32_t n = T.ncompact;
+    uint32_t off = 0, n = 0;
+#pragma unroll
+    for (int w = 0; w < SCAN_THREADS / WAVE; ++w) {
+        off += w < wv ? T.wave_cnt[w] : 0u;
+        n += T.wave_cnt[w];
+    }
+    if (live) T.compact[off + rank] = (uint16_t)tid;
+    if (tid == 0) T.ncompact = n;
+    __syncthreads();
     if (tid == 0 && n) {
         T.base = atomicAdd(&C->n_records, (unsigned long long)n);
         atomicMax(&C->max_v, T.maxv);
@@ -217,18 +236,17 @@ constexpr int WG_ROWS = ROWS * WAVES;                     // 32 = tile y extent
 constexpr uint32_t MARK_ADJ = 0xFFFFFFFFu;                // stage entry: nearest-neighbour face, no sample
 constexpr uint32_t MARK_ONE = 0xFFFFFFFEu;                // stage entry: one affinity sample in .z
 
+// canonical (min, max) key, branch free; with 64-bit labels a label >= 2^32
+// deactivates the face and raises the lane's overflow flag
 template <typename LabelT>
-__device__ __forceinline__ bool make_key(LabelT a, LabelT b, uint64_t& key, bool& ovf) {
+__device__ __forceinline__ bool make_key(bool act, LabelT a, LabelT b, uint64_t& key, bool& ovf) {
     const LabelT u = a < b ? a : b;
     const LabelT v = a < b ? b : a;
-    if constexpr (sizeof(LabelT) == 8) {
-        if (v >> 32) {
-            ovf = true;
-            return false;
-        }
-    }
-    key = ((uint64_t)u << 32) | (uint64_t)v;
-    return true;
+    bool bad = false;
+    if constexpr (sizeof(LabelT) == 8) bad = (v >> 32) != 0;
+    ovf = ovf | (act & bad);
+    key = ((uint64_t)u << 32) | (uint64_t)(uint32_t)v;
+    return act & !bad;
 }
 
 // Compacted face stream.  Each site (one row of one face axis) contributes
@@ -239,18 +257,44 @@ __device__ __forceinline__ bool make_key(LabelT a, LabelT b, uint64_t& key, bool
 // lane of a batch carries a face, instead of ~1 in 10 lanes of a site.
 template <int MODE>
 __device__ __forceinline__ void fold_batch(Table& T, const uint4* __restrict__ stage, int nb, int lane, RecordBuf R,
-                                           Counters* C, bool fast40, double scale, double offset) {
+                                           Counters* C, bool fast40, double scale, double offset, int ablate) {
     constexpr bool BND = MODE == MODE_BOUNDARY;
     constexpr bool AFF = MODE == MODE_AFFINITY;
     constexpr bool STATS = MODE != MODE_GRAPH;
     if (lane >= nb) return;
     const uint4 e = stage[lane];
+    if (ablate & 32) {   // diagnostic: no fold
+        if (e.x == 0x12345u && e.y == 0x6789u) atomicAdd(&C->pad[1], 1ull);
+        return;
+    }
     const uint64_t key = ((uint64_t)e.y << 32) | e.x;
     const uint32_t h = home_bucket(key);
-    const uint4 bk = *reinterpret_cast<const uint4*>(&T.key[h]);
-    const uint64_t k0 = ((uint64_t)bk.y << 32) | bk.x;
-    const uint64_t k1 = ((uint64_t)bk.w << 32) | bk.z;
-    const int s = k0 == key ? (int)h : (k1 == key ? (int)h + 1 : table_insert(T, key));
+    const uint4 b01 = *reinterpret_cast<const uint4*>(&T.key[h]);
+    const uint4 b23 = *reinterpret_cast<const uint4*>(&T.key[h + 2]);
+    const uint64_t kk[4] = {((uint64_t)b01.y << 32) | b01.x, ((uint64_t)b01.w << 32) | b01.z,
+                            ((uint64_t)b23.y << 32) | b23.x, ((uint64_t)b23.w << 32) | b23.z};
+    int s = -1, empty = -1;
+#pragma unroll
+    for (int j = 3; j >= 0; --j) {
+        s = kk[j] == key ? (int)h + j : s;
+        empty = kk[j] == EMPTY_KEY ? j : empty;
+    }
+    if (s < 0) {
+        // not in the home bucket: claim its first empty slot with one CAS
+        // (the probe order is linear from the bucket start, so the key cannot
+        // sit beyond an empty slot); a lost race or a full bucket probes on
+        bool done = false;
+        if (empty >= 0) {
+            const uint64_t old = atomicCAS((unsigned long long*)&T.key[h + empty], (unsigned long long)EMPTY_KEY,
+                                           (unsigned long long)key);
+            if (old == EMPTY_KEY) atomicAdd(&T.used, 1u);
+            if (old == EMPTY_KEY || old == key) {
+                s = (int)h + empty;
+                done = true;
+            }
+        }
+        if (!done) s = table_insert(T, key);
+    }
     const float a = __uint_as_float(e.z), b = __uint_as_float(e.w);
     if (s < 0) {
         if constexpr (BND) emit_direct(R, C, key, 2, a, b, scale, offset, 0u, true);
@@ -261,12 +305,17 @@ __device__ __forceinline__ void fold_batch(Table& T, const uint4* __restrict__ s
         if constexpr (!STATS) emit_direct(R, C, key, 0, 0.f, 0.f, scale, offset, 0u, false);
         return;
     }
+    if (ablate & 64) {   // diagnostic: probe only
+        if (s == 0x7FFFFFFF) atomicAdd(&C->pad[1], 1ull);
+        return;
+    }
     if constexpr (BND) {
         atomicAdd(&T.w[s][21], 2u);
         atomicAdd(&T.sum[s], (double)a + (double)b);
         atomicAdd(&T.sq[s], (double)a * (double)a + (double)b * (double)b);
         atomicMin(&T.w[s][22], f2ord(fminf(a, b)));
         atomicMax(&T.w[s][23], f2ord(fmaxf(a, b)));
+        if (ablate & 128) return;   // diagnostic: no histogram
         hist_add(T, s, sample_slot(a, fast40, scale, offset));
         hist_add(T, s, sample_slot(b, fast40, scale, offset));
     }
@@ -287,7 +336,9 @@ __device__ __forceinline__ void fold_batch(Table& T, const uint4* __restrict__ s
 template <typename LabelT, typename DataT, int MODE>
 __global__ __launch_bounds__(SCAN_THREADS, 4) void k_face_scan(ScanParams P, RecordBuf R, Counters* C) {
     __shared__ Table T;
-    __shared__ uint4 stage_all[SCAN_THREADS / WAVE][WAVE];
+    // per-wave stage: 64 live entries + 64 slots where inactive lanes park
+    // their (unconditional, branch-free) store
+    __shared__ uint4 stage_all[SCAN_THREADS / WAVE][2 * WAVE];
     constexpr bool STATS = MODE != MODE_GRAPH;
     constexpr bool BND = MODE == MODE_BOUNDARY;
     constexpr bool AFF = MODE == MODE_AFFINITY;
@@ -352,26 +403,33 @@ __global__ __launch_bounds__(SCAN_THREADS, 4) void k_face_scan(ScanParams P, Rec
     };
 
     const int ablate = P.ablate;
+    // diagnostic (ablate & 256): shader-clock stamps per phase, summed per wave
+    const bool stamps = (ablate & 256) != 0;
+    uint64_t t_fold = 0, t_flush = 0, t_check = 0, t_start = stamps ? __builtin_amdgcn_s_memtime() : 0;
     uint64_t chk = 0;
     bool ovf = false;
     int nbuf = 0;   // staged faces (wave-uniform)
 
     auto flush_stage = [&]() {
         if (nbuf) {
-            fold_batch<MODE>(T, stage, nbuf, lane, R, C, fast40, scale, offset);
+            const uint64_t t0 = stamps ? __builtin_amdgcn_s_memtime() : 0;
+            fold_batch<MODE>(T, stage, nbuf, lane, R, C, fast40, scale, offset, ablate);
+            if (stamps) {
+                __builtin_amdgcn_s_waitcnt(0);
+                t_fold += __builtin_amdgcn_s_memtime() - t0;
+            }
             nbuf = 0;
         }
     };
     // append the active lanes of one site to the stage
     auto push = [&](bool act, uint64_t key, float a, uint32_t bbits) {
         const uint64_t m = __ballot(act);
-        if (m == 0) return;
         const int k = __popcll(m);
         if (nbuf + k > WAVE) flush_stage();
-        if (act) {
-            const int rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
-            stage[nbuf + rank] = make_uint4((uint32_t)key, (uint32_t)(key >> 32), __float_as_uint(a), bbits);
-        }
+        // active lanes append at nbuf + rank; inactive lanes park behind them
+        const int rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+        const int pos = act ? nbuf + rank : nbuf + k + (lane - rank);
+        stage[pos] = make_uint4((uint32_t)key, (uint32_t)(key >> 32), __float_as_uint(a), bbits);
         nbuf += k;
     };
     auto face_bits = [&](float b) -> uint32_t { return AFF ? MARK_ADJ : __float_as_uint(b); };
@@ -404,11 +462,11 @@ __global__ __launch_bounds__(SCAN_THREADS, 4) void k_face_scan(ScanParams P, Rec
                 }
                 uint64_t key = 0;
                 bool act = y < Y && inx && hx && own_z_lo && own_y_lo && own_x_up && lc != lx;
-                if (act) act = make_key<LabelT>(lc, lx, key, ovf);
+                act = make_key<LabelT>(act, lc, lx, key, ovf);
                 push(act, key, Dc[r], face_bits(dx));
                 // y face (y, y+1)
                 act = y + 1 < Y && inx && own_z_lo && own_y_up && own_x_lo && lc != Lc[r + 1];
-                if (act) act = make_key<LabelT>(lc, Lc[r + 1], key, ovf);
+                act = make_key<LabelT>(act, lc, Lc[r + 1], key, ovf);
                 push(act, key, Dc[r], face_bits(Dc[r + 1]));
                 // affinity samples aff[c, p] for q = p + o_c, p in the owned box
                 if constexpr (AFF) {
@@ -426,7 +484,7 @@ __global__ __launch_bounds__(SCAN_THREADS, 4) void k_face_scan(ScanParams P, Rec
                             av = load_val<DataT>(D, (int64_t)c * Z * sz + i);
                         }
                         bool sact = inq && lq != lc;
-                        if (sact) sact = make_key<LabelT>(lc, lq, key, ovf);
+                        sact = make_key<LabelT>(sact, lc, lq, key, ovf);
                         push(sact, key, av, MARK_ONE);
                     }
                 }
@@ -439,21 +497,29 @@ __global__ __launch_bounds__(SCAN_THREADS, 4) void k_face_scan(ScanParams P, Rec
                     const bool own_y_lo = y >= oby && y < oey;
                     uint64_t key = 0;
                     bool act = y < Y && inx && own_z_up && own_y_lo && own_x_lo && Lc[r] != Ln[r];
-                    if (act) act = make_key<LabelT>(Lc[r], Ln[r], key, ovf);
+                    act = make_key<LabelT>(act, Lc[r], Ln[r], key, ovf);
                     push(act, key, Dc[r], face_bits(Dn[r]));
                 }
             }
         }
-        // plane done: fold the staged faces (exact counts for the u16 guard),
-        // then decide on a flush
-        flush_stage();
-        if (!(ablate & 16)) {
+        // every CHECK_PLANES planes: decide on a flush.  Staged faces stay
+        // staged (raw faces are valid for whatever table they are folded into
+        // later); hist_guard leaves room for them and for CHECK_PLANES planes
+        // in the u16 slot bound, the fill threshold leaves room for the new
+        // keys of CHECK_PLANES planes (a full table still falls back to
+        // direct records).
+        if (!(ablate & 16) && ((z - z0) % P.check_planes == P.check_planes - 1 || z + 1 == z1)) {
+            const uint64_t t2 = stamps ? __builtin_amdgcn_s_memtime() : 0;
             __syncthreads();
-            bool need = tid == 0 && T.used > TABLE_CAP / 2;
+            if (stamps) t_check += __builtin_amdgcn_s_memtime() - t2;
+            bool need = tid == 0 && T.used > TABLE_CAP * 3 / 8;
             if constexpr (STATS) {
                 for (int e = tid; e < TABLE_CAP; e += SCAN_THREADS) need |= (T.w[e][21] & ~ADJ_FLAG) > P.hist_guard;
             }
-            if (__syncthreads_or(need)) table_flush<MODE>(T, R, C);
+            const bool do_flush = __syncthreads_or(need);
+            const uint64_t t1 = stamps ? __builtin_amdgcn_s_memtime() : 0;
+            if (do_flush) table_flush<MODE>(T, R, C);
+            if (stamps) t_flush += __builtin_amdgcn_s_memtime() - t1;
         }
 #pragma unroll
         for (int r = 0; r <= ROWS; ++r) {
@@ -467,6 +533,12 @@ __global__ __launch_bounds__(SCAN_THREADS, 4) void k_face_scan(ScanParams P, Rec
         if (chk == 0x9E3779B97F4A7C15ull) atomicAdd(&C->pad[0], 1ull);
     }
     if (__ballot(ovf) && lane == 0) atomicAdd(&C->label_overflow, 1ull);
+    if (stamps && lane == 0) {
+        atomicAdd(&C->pad[2], (unsigned long long)t_fold);
+        atomicAdd(&C->pad[3], (unsigned long long)t_flush);
+        atomicAdd((unsigned long long*)&C->pad[1], (unsigned long long)t_check);
+        atomicAdd(&C->pad[0], (unsigned long long)(__builtin_amdgcn_s_memtime() - t_start));
+    }
     flush_stage();
     table_flush<MODE>(T, R, C);
 }

@@ -22,6 +22,6 @@ if len(sys.argv) > 1:
         r.free()
     print(json.dumps({'ablate': mode, **out}), flush=True)
 else:
-    for ab in ['0', '8']:
+    for ab in ['0', '8', '32', '64', '128']:
         env = dict(os.environ, CTG_ABLATE=ab)
         subprocess.run([sys.executable, __file__, ab], env=env, check=True)
