@@ -19,6 +19,8 @@ CTG_MEM_DEVICE = 1
 CTG_DATA_NONE = 0
 CTG_DATA_F32 = 1
 CTG_DATA_U8 = 2
+CTG_KEEP_STATS = 1
+CTG_NO_ADJ_FILTER = 2
 CTG_MAX_CHANNELS = 24
 CTG_N_FEATURES = 10
 CTG_NBINS = 40
@@ -47,6 +49,7 @@ PROTOTYPES = {
     'ctg_merge_stats': (ctypes.c_int, [c_vp, c_vp, c_vp, ctypes.c_int64, ctypes.c_double, ctypes.c_double,
                                        ctypes.c_int, ctypes.c_int, c_vp, ctypes.POINTER(c_vp)]),
     'ctg_unique_pairs': (ctypes.c_int, [c_vp, ctypes.c_int64, ctypes.c_int, c_vp, ctypes.POINTER(c_vp)]),
+    'ctg_unique_values': (ctypes.c_int, [c_vp, ctypes.c_int64, ctypes.c_int, c_vp, ctypes.POINTER(c_vp)]),
     'ctg_map_edge_ids': (ctypes.c_int, [c_vp, ctypes.c_int64, c_vp, ctypes.c_int64, c_vp, ctypes.c_int, c_vp]),
     'ctg_result_num_edges': (ctypes.c_int64, [c_vp]),
     'ctg_result_num_nodes': (ctypes.c_int64, [c_vp]),

@@ -37,6 +37,11 @@ hipError_t launch_find_edges(const uint64_t* ge, int64_t n, const uint64_t* q, i
 hipError_t launch_synth(uint64_t* labels, float* boundary, const int64_t* shape, int64_t z_offset,
                         const int64_t* gshape, int cell, uint64_t seed, uint64_t label_offset, double noise_amp,
                         hipStream_t s);
+hipError_t launch_remap_dense(const uint64_t* L, int64_t V, const uint64_t* U, int64_t n, uint32_t* out,
+                              hipStream_t s);
+hipError_t launch_gather_labels(const uint64_t* U, uint64_t* x, int64_t n, hipStream_t s);
+hipError_t launch_remap_dense64(const uint64_t* L, int64_t V, const uint64_t* U, int64_t n, uint64_t* out,
+                                hipStream_t s);
 hipError_t launch_synth_aff(const float* b, float* out, const int64_t* shape, int n_channels, const int32_t* off,
                             hipStream_t s);
 
@@ -393,10 +398,80 @@ static int stage_in(Workspace& w, int slot, const void* src, size_t bytes, int m
     return CTG_OK;
 }
 
+// (u,v) pair lists with labels >= 2^32 (merge / union inputs): the sort packs
+// (u,v) into one 64-bit key, so the endpoints are replaced by their rank in
+// the sorted unique endpoint table (monotone) and mapped back afterwards.
+struct DensePairs {
+    ctg_result* U = nullptr;
+    uint64_t* dense = nullptr;
+    int build(const uint64_t* dk, int64_t n, hipStream_t s) {
+        int rc = ctg_unique_values(dk, 2 * n, CTG_MEM_DEVICE, s, &U);
+        if (rc) return rc;
+        dense = (uint64_t*)dalloc((size_t)n * 16);
+        if (!dense) {
+            set_error("out of device memory for the dense endpoint relabelling");
+            return CTG_ERR_NOMEM;
+        }
+        CTG_CHECK(launch_remap_dense64(dk, 2 * n, U->nodes, U->n_nodes, dense, s));
+        return CTG_OK;
+    }
+    hipError_t map_back(ctg_result* r, hipStream_t s) {
+        if (!U) return hipSuccess;
+        hipError_t e = launch_gather_labels(U->nodes, r->edges, 2 * r->n_edges, s);
+        if (e == hipSuccess) e = launch_gather_labels(U->nodes, r->nodes, r->n_nodes, s);
+        return e;
+    }
+    ~DensePairs() {
+        if (dense) dfree(dense);   // stream-ordered reuse
+        if (U) ctg_free(U);
+    }
+};
+
+// Labels >= 2^32: the face keys pack (u,v) as 32+32 bits, so the
+// array is relabelled densely through its sorted unique labels (a monotone
+// map: sorted dense edges stay sorted), scanned as 32-bit labels, and the
+// edge and node tables are mapped back.
+static int rag_dense_relabel(const void* dl, const void* dd, int data_kind, int n_channels, const int32_t* offsets,
+                             const int64_t* shape, const int64_t* own_begin, const int64_t* own_end,
+                             int ignore_label, double hist_lo, double hist_hi, int flags, void* stream,
+                             ctg_result** out) {
+    hipStream_t s = (hipStream_t)stream;
+    ctg_result* U = nullptr;
+    int rc = ctg_unique_labels((const uint64_t*)dl, shape, nullptr, nullptr, CTG_MEM_DEVICE, stream, &U);
+    if (rc) return rc;
+    if (U->n_nodes > 0xFFFFFFFFll) {
+        ctg_free(U);
+        set_error("ctg_rag_features: more than 2^32 distinct labels in one array");
+        return CTG_ERR_UNSUPPORTED;
+    }
+    const int64_t V = shape[0] * shape[1] * shape[2];
+    uint32_t* dense = (uint32_t*)dalloc((size_t)V * 4);
+    if (!dense) {
+        ctg_free(U);
+        set_error("ctg_rag_features: out of device memory for the dense relabelling");
+        return CTG_ERR_NOMEM;
+    }
+    CTG_CHECK(launch_remap_dense((const uint64_t*)dl, V, U->nodes, U->n_nodes, dense, s));
+    ctg_result* r = nullptr;
+    rc = ctg_rag_features(dense, 32, dd, data_kind, n_channels, offsets, shape, own_begin, own_end, ignore_label,
+                          hist_lo, hist_hi, flags, CTG_MEM_DEVICE, stream, &r);
+    dfree(dense);   // stream-ordered: later users of the block run after the scan
+    if (rc) {
+        ctg_free(U);
+        return rc;
+    }
+    CTG_CHECK(launch_gather_labels(U->nodes, r->edges, 2 * r->n_edges, s));
+    CTG_CHECK(launch_gather_labels(U->nodes, r->nodes, r->n_nodes, s));
+    CTG_CHECK(hipStreamSynchronize(s));
+    ctg_free(U);
+    *out = r;
+    return CTG_OK;
+}
+
 int ctg_rag_features(const void* labels, int label_bits, const void* data, int data_kind, int n_channels,
                      const int32_t* offsets, const int64_t* shape, const int64_t* own_begin,
                      const int64_t* own_end, int ignore_label,
-                     double hist_lo, double hist_hi, int keep_stats, int mem, void* stream, ctg_result** out) {
+                     double hist_lo, double hist_hi, int flags, int mem, void* stream, ctg_result** out) {
     if (!out || !shape || !labels) {
         set_error("ctg_rag_features: null argument");
         return CTG_ERR_ARG;
@@ -496,9 +571,12 @@ int ctg_rag_features(const void* labels, int label_bits, const void* data, int d
         CTG_CHECK(hipMemcpyAsync(w.counters_host, w.counters, sizeof(Counters), hipMemcpyDeviceToHost, s));
         CTG_CHECK(hipStreamSynchronize(s));
         if (w.counters_host->label_overflow) {
-            set_error("ctg_rag_features: labels >= 2^32 need label_bits=32 after dense relabelling "
-                      "(use ctg_unique_labels + remap)");
-            return CTG_ERR_UNSUPPORTED;
+            if (label_bits != 64) {
+                set_error("ctg_rag_features: internal label overflow on 32-bit labels");
+                return CTG_ERR_HIP;
+            }
+            return rag_dense_relabel(dl, dd, data_kind, n_channels, offsets, shape, own_begin, own_end,
+                                     ignore_label, hist_lo, hist_hi, flags, stream, out);
         }
         if ((int64_t)w.counters_host->n_records <= w.rec.cap) break;
         need = (int64_t)(w.counters_host->n_records * 5 / 4) + 1024;
@@ -524,9 +602,9 @@ int ctg_rag_features(const void* labels, int label_bits, const void* data, int d
     J.R = w.rec;
     J.wide = 0;
     J.stats = stats;
-    J.need_adj = P.n_channels > 0 ? 1 : 0;
+    J.need_adj = P.n_channels > 0 ? ((flags & CTG_NO_ADJ_FILTER) ? 2 : 1) : 0;
     J.ignore_label = ignore_label;
-    J.keep_stats = keep_stats;
+    J.keep_stats = (flags & CTG_KEEP_STATS) ? 1 : 0;
     J.max_v = w.counters_host->max_v;
     J.scale = P.scale;
     J.offset = P.offset;
@@ -642,6 +720,54 @@ int ctg_unique_labels(const uint64_t* labels, const int64_t* shape, const int64_
     return CTG_ERR_NOMEM;
 }
 
+int ctg_unique_values(const uint64_t* values, int64_t n, int mem, void* stream, ctg_result** out) {
+    if (!out || n < 0 || (n > 0 && !values)) {
+        set_error("ctg_unique_values: bad arguments");
+        return CTG_ERR_ARG;
+    }
+    *out = nullptr;
+    const int dev = cur_dev();
+    Workspace& w = ws(dev);
+    CTG_CHECK(ws_init(w));
+    hipStream_t s = (hipStream_t)stream;
+    ctg_result* r = new ctg_result();
+    r->device = dev;
+    r->edges = (uint64_t*)dalloc(16);
+    r->nodes = (uint64_t*)dalloc(std::max<int64_t>(n, 1) * 8);
+    if (n == 0) {
+        *out = r;
+        return CTG_OK;
+    }
+    uint64_t* in = (uint64_t*)values;
+    uint64_t* sorted = (uint64_t*)dalloc(n * 8);
+    if (mem == CTG_MEM_HOST) in = (uint64_t*)dalloc(n * 8);
+    if (!in || !sorted || !r->nodes) {
+        set_error("ctg_unique_values: out of device memory");
+        ctg_free(r);
+        return CTG_ERR_NOMEM;
+    }
+    if (mem == CTG_MEM_HOST) CTG_CHECK(hipMemcpyAsync(in, values, n * 8, hipMemcpyHostToDevice, s));
+    size_t tb = 0;
+    CTG_CHECK(rocprim::radix_sort_keys(nullptr, tb, in, sorted, (size_t)n, 0u, 64u, s));
+    ensure(&w.temp, w.temp_bytes, tb + 256);
+    tb = w.temp_bytes;
+    CTG_CHECK(rocprim::radix_sort_keys(w.temp, tb, in, sorted, (size_t)n, 0u, 64u, s));
+    tb = 0;
+    CTG_CHECK(rocprim::unique(nullptr, tb, sorted, r->nodes, w.small + 2, (size_t)n,
+                              rocprim::equal_to<uint64_t>(), s));
+    ensure(&w.temp, w.temp_bytes, tb + 256);
+    tb = w.temp_bytes;
+    CTG_CHECK(rocprim::unique(w.temp, tb, sorted, r->nodes, w.small + 2, (size_t)n,
+                              rocprim::equal_to<uint64_t>(), s));
+    CTG_CHECK(hipMemcpyAsync(w.small_host + 2, w.small + 2, 4, hipMemcpyDeviceToHost, s));
+    CTG_CHECK(hipStreamSynchronize(s));
+    r->n_nodes = w.small_host[2];
+    dfree(sorted);
+    if (mem == CTG_MEM_HOST) dfree(in);
+    *out = r;
+    return CTG_OK;
+}
+
 int ctg_merge_stats(const uint64_t* keys, const double* sums, const uint32_t* records, int64_t n, double hist_lo,
                     double hist_hi, int keep_stats, int mem, void* stream, ctg_result** out) {
     if (!out || n < 0 || (n > 0 && (!keys || !sums || !records))) {
@@ -683,14 +809,17 @@ int ctg_merge_stats(const uint64_t* keys, const double* sums, const uint32_t* re
     CTG_CHECK(launch_max_pairs(n, dk, &w.counters->max_v, s));
     CTG_CHECK(hipMemcpyAsync(w.counters_host, w.counters, sizeof(Counters), hipMemcpyDeviceToHost, s));
     CTG_CHECK(hipStreamSynchronize(s));
+    DensePairs dp;
     if (w.counters_host->max_v >> 32) {
-        set_error("ctg_merge_stats: labels >= 2^32 are not supported by the merge");
-        delete r;
-        return CTG_ERR_UNSUPPORTED;
+        int rc = dp.build(dk, n, s);
+        if (rc) {
+            delete r;
+            return rc;
+        }
     }
     ReduceJob J{};
     J.n = n;
-    J.pairs = dk;
+    J.pairs = dp.U ? dp.dense : dk;
     J.R.key = nullptr;
     J.R.sums = ds;
     J.R.hist = dr;
@@ -700,10 +829,11 @@ int ctg_merge_stats(const uint64_t* keys, const double* sums, const uint32_t* re
     J.need_adj = 1;
     J.ignore_label = 0;
     J.keep_stats = keep_stats;
-    J.max_v = w.counters_host->max_v;
+    J.max_v = dp.U ? (uint64_t)std::max<int64_t>(dp.U->n_nodes - 1, 0) : w.counters_host->max_v;
     J.scale = (double)NBINS / (hist_hi - hist_lo);
     J.offset = hist_lo;
     hipError_t e = reduce_records(w, J, s, r);
+    if (e == hipSuccess) e = dp.map_back(r, s);
     if (e == hipSuccess) e = hipStreamSynchronize(s);
     if (owned) {
         dfree(dk);
@@ -751,21 +881,25 @@ int ctg_unique_pairs(const uint64_t* pairs, int64_t n, int mem, void* stream, ct
     CTG_CHECK(launch_max_pairs(n, dk, &w.counters->max_v, s));
     CTG_CHECK(hipMemcpyAsync(w.counters_host, w.counters, sizeof(Counters), hipMemcpyDeviceToHost, s));
     CTG_CHECK(hipStreamSynchronize(s));
+    DensePairs dp;
     if (w.counters_host->max_v >> 32) {
-        set_error("ctg_unique_pairs: labels >= 2^32 are not supported");
-        if (mem == CTG_MEM_HOST) dfree(dk);
-        delete r;
-        return CTG_ERR_UNSUPPORTED;
+        int rc = dp.build(dk, n, s);
+        if (rc) {
+            if (mem == CTG_MEM_HOST) dfree(dk);
+            delete r;
+            return rc;
+        }
     }
     ReduceJob J{};
     J.n = n;
-    J.pairs = dk;
+    J.pairs = dp.U ? dp.dense : dk;
     J.stats = 0;
     J.need_adj = 0;
-    J.max_v = w.counters_host->max_v;
+    J.max_v = dp.U ? (uint64_t)std::max<int64_t>(dp.U->n_nodes - 1, 0) : w.counters_host->max_v;
     J.scale = 1.0;
     J.offset = 0.0;
     hipError_t e = reduce_records(w, J, s, r);
+    if (e == hipSuccess) e = dp.map_back(r, s);
     if (e == hipSuccess) e = hipStreamSynchronize(s);
     if (mem == CTG_MEM_HOST) dfree(dk);
     if (e != hipSuccess) {

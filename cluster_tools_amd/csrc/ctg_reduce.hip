@@ -9,6 +9,8 @@
 // Column contract (E,10): mean, var, min, q10, q25, q50, q75, q90, max, count
 // (features/block_edge_features.py:146-147, features/merge_edge_features.py:62-65,
 // costs/probs_to_costs.py:205-207).
+#include <algorithm>
+
 #include "ctg_internal.h"
 
 namespace ctg {
@@ -169,7 +171,7 @@ __global__ __launch_bounds__(256) void k_reduce_edges(int64_t E, const uint64_t*
         } else {
             flags = ADJ_FLAG;
         }
-        if (O.keep) O.keep[e] = ((flags & ADJ_FLAG) || !need_adj) && !(ignore_label && u == 0) ? 1u : 0u;
+        if (O.keep) O.keep[e] = ((flags & ADJ_FLAG) || need_adj != 1) && !(ignore_label && u == 0) ? 1u : 0u;
         return;
     } else {
         uint32_t h[NSLOTS];
@@ -185,8 +187,10 @@ __global__ __launch_bounds__(256) void k_reduce_edges(int64_t E, const uint64_t*
             sum += s.x;
             sq += s.y;
         }
-        if (!need_adj) flags |= ADJ_FLAG;
-        const bool keep = (flags & ADJ_FLAG) && !(ignore_label && u == 0);
+        // need_adj: 0 every record is an edge (boundary maps), 1 keep edges seen
+        // on a nearest-neighbour face, 2 keep all and carry the flag (partials)
+        if (need_adj == 0) flags |= ADJ_FLAG;
+        const bool keep = (need_adj == 2 || (flags & ADJ_FLAG)) && !(ignore_label && u == 0);
         if (O.keep) O.keep[e] = keep ? 1u : 0u;
         if (O.wstats) {
             uint4* p = (uint4*)(O.wstats + (size_t)e * WREC_WORDS);
@@ -317,6 +321,50 @@ __global__ void k_find_edges(const uint64_t* __restrict__ ge, int64_t n, const u
         else hi = mid;
     }
     out[i] = (lo < n && ge[2 * lo] == qu && ge[2 * lo + 1] == qv) ? lo : -1;
+}
+
+// labels >= 2^32: dense relabelling through the sorted unique label table U
+// (monotone, so sorted dense edges stay sorted after mapping back)
+template <typename OutT>
+__global__ void k_remap_dense(const uint64_t* __restrict__ L, int64_t V, const uint64_t* __restrict__ U, int64_t n,
+                              OutT* __restrict__ out) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < V; i += (int64_t)gridDim.x * blockDim.x) {
+        const uint64_t x = L[i];
+        int64_t lo = 0, hi = n;
+        while (lo < hi) {
+            const int64_t mid = (lo + hi) >> 1;
+            if (U[mid] < x) lo = mid + 1;
+            else hi = mid;
+        }
+        out[i] = (OutT)lo;
+    }
+}
+
+__global__ void k_gather_labels(const uint64_t* __restrict__ U, uint64_t* __restrict__ x, int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) x[i] = U[x[i]];
+}
+
+hipError_t launch_remap_dense(const uint64_t* L, int64_t V, const uint64_t* U, int64_t n, uint32_t* out,
+                              hipStream_t s) {
+    if (V == 0) return hipSuccess;
+    const int64_t blocks = std::min<int64_t>((V + 255) / 256, 256 * 64);
+    hipLaunchKernelGGL(k_remap_dense<uint32_t>, dim3((unsigned)blocks), dim3(256), 0, s, L, V, U, n, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_remap_dense64(const uint64_t* L, int64_t V, const uint64_t* U, int64_t n, uint64_t* out,
+                                hipStream_t s) {
+    if (V == 0) return hipSuccess;
+    const int64_t blocks = std::min<int64_t>((V + 255) / 256, 256 * 64);
+    hipLaunchKernelGGL(k_remap_dense<uint64_t>, dim3((unsigned)blocks), dim3(256), 0, s, L, V, U, n, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_gather_labels(const uint64_t* U, uint64_t* x, int64_t n, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_gather_labels, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, U, x, n);
+    return hipGetLastError();
 }
 
 hipError_t launch_pack_keys(int64_t n, const uint64_t* key, int nb, uint64_t* sk, uint32_t* idx, hipStream_t s) {

@@ -1,0 +1,215 @@
+"""Multi-GPU RAG + edge features: one process per GPU, z-slabs, RCCL exchange.
+
+This is the MI355X replacement for the reference's block -> merge structure
+at the scale of whole GPUs.  In the reference a volume is cut into blocks,
+``initial_sub_graphs`` / ``block_edge_features`` run per block and
+``merge_sub_graphs`` / ``merge_edge_features`` combine the per-block results
+(graph/merge_sub_graphs.py:130-135, features/merge_edge_features.py:141-147).
+Here every rank owns one z-slab that is resident in its HBM (288 GB per GPU
+holds slabs of several Gvoxels), reads one halo plane below it, and runs the
+single-launch face scan over the whole slab with ``keep_stats`` so that its
+per-edge partial statistics stay mergeable.  The only exchange step of the
+path is the merge: edges are range-partitioned by their lower label ``u``
+(splitters from an all-gathered sample, so the concatenation of the rank
+shards is the globally sorted edge table), the partial rows travel in one
+``all_to_all_single`` (28 x int64 per edge: (u,v), (sum, sumsq), the 48-word
+wide record) and each rank merges what it received with ``ctg_merge_stats``.
+Node lists take the same route.  Scaling is weak: per-rank slab size is fixed.
+
+The exchange logic is backend-agnostic: ``HipBackend`` (libctg.so, the
+product path) or, in the CPU tests, an oracle-backed numpy backend with the
+same three methods, which lets the partition/exchange code run under gloo.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROW_WORDS = 28            # int64 words per exchanged edge row
+WIDE_WORDS = 48           # u32 words of one wide statistics record
+N_SAMPLES = 4096          # splitter sample per rank
+
+
+class HipBackend:
+    """Local partial tables and the merge on the GPU through libctg.so."""
+
+    def local(self, labels, data, offsets, own_begin, own_end, ignore_label, hist_range):
+        from . import rag
+        # affinity partials keep non-adjacent pairs: adjacency is only known
+        # globally, after the merge ORs the ADJ bits of all slabs
+        r = rag.rag_features_handle(labels, data, offsets=offsets, own_begin=own_begin, own_end=own_end,
+                                    ignore_label=ignore_label, hist_range=hist_range, keep_stats=True,
+                                    no_adj_filter=offsets is not None)
+        keys = r.edges_torch_i64()
+        sums, recs = r.stats_torch()
+        nodes = r.nodes_torch()
+        info = r.info()
+        r.free()
+        return keys, sums, recs, nodes, info
+
+    def merge(self, keys, sums, recs, hist_range):
+        from . import rag
+        return rag.merge_stats_handle(keys, sums, recs, hist_range=hist_range)
+
+    def unique(self, values):
+        from . import rag
+        r = rag.unique_values_handle(values)
+        out = r.nodes_torch()
+        r.free()
+        return out
+
+
+def pack_rows(keys, sums, recs):
+    """(E,2) int64 keys, (E,2) float64 sums, (E,48) int32 records -> (E,28) int64."""
+    n = keys.shape[0]
+    return torch.cat([keys.reshape(n, 2), sums.reshape(n, 2).view(torch.int64),
+                      recs.reshape(n, WIDE_WORDS).view(torch.int64)], dim=1)
+
+
+def unpack_rows(rows):
+    rows = rows.reshape(-1, ROW_WORDS)
+    keys = rows[:, :2].contiguous()
+    sums = rows[:, 2:4].contiguous().view(torch.float64)
+    recs = rows[:, 4:].contiguous().view(torch.int32)
+    return keys, sums, recs
+
+
+def weighted_splitters(samples, counts, world):
+    """Range splitters (world-1 values) from per-rank samples of sorted keys.
+
+    samples: (world, S) int64, row r an evenly spaced sample of rank r's sorted
+    keys (meaningless where counts[r] == 0); counts: (world,) key totals.  Each
+    sample of rank r stands for counts[r]/S keys.  Deterministic, so every
+    rank computes the same splitters from the same gathered data.
+    """
+    samples = np.asarray(samples, dtype=np.int64)
+    counts = np.asarray(counts, dtype=np.float64)
+    S = samples.shape[1]
+    w = np.repeat(counts / S, S)
+    v = samples.reshape(-1)
+    keep = w > 0
+    v, w = v[keep], w[keep]
+    if v.size == 0:
+        return np.zeros(world - 1, dtype=np.int64)
+    order = np.argsort(v, kind='stable')
+    v, w = v[order], w[order]
+    cw = np.cumsum(w)
+    total = cw[-1]
+    targets = total * np.arange(1, world) / world
+    idx = np.minimum(np.searchsorted(cw, targets, side='left'), v.size - 1)
+    return v[idx].astype(np.int64)
+
+
+def split_counts(sorted_keys, splitters):
+    """Rows per destination rank for a key column sorted ascending:
+    rank k gets splitters[k-1] <= key < splitters[k]."""
+    n = sorted_keys.shape[0]
+    if len(splitters) == 0:
+        return [n]
+    sp = torch.as_tensor(np.asarray(splitters), dtype=torch.int64, device=sorted_keys.device)
+    pos = torch.searchsorted(sorted_keys.contiguous(), sp, right=False).cpu().tolist()
+    bounds = [0] + pos + [n]
+    return [bounds[i + 1] - bounds[i] for i in range(len(bounds) - 1)]
+
+
+def exchange(rows, send_counts, group=None):
+    """all_to_all of variable-length row blocks; returns the received rows."""
+    world = dist.get_world_size(group)
+    dev = rows.device
+    sc = torch.tensor(send_counts, dtype=torch.int64, device=dev)
+    rc = torch.empty(world, dtype=torch.int64, device=dev)
+    dist.all_to_all_single(rc, sc, group=group)
+    recv_counts = rc.cpu().tolist()
+    shape = (sum(recv_counts),) + tuple(rows.shape[1:])
+    out = torch.empty(shape, dtype=rows.dtype, device=dev)
+    dist.all_to_all_single(out, rows.contiguous(), output_split_sizes=recv_counts,
+                           input_split_sizes=list(send_counts), group=group)
+    return out
+
+
+class DistResult:
+    """This rank's shard of the global (sorted) edge table + features + nodes."""
+
+    def __init__(self, merged, nodes, edge_offset, n_edges_global, node_offset, n_nodes_global, info):
+        self.merged = merged          # backend merge result (rag.Result or dict)
+        self.node_shard = nodes
+        self.edge_offset = edge_offset
+        self.n_edges_global = n_edges_global
+        self.node_offset = node_offset
+        self.n_nodes_global = n_nodes_global
+        self._info = info
+
+    @property
+    def n_edges(self):
+        m = self.merged
+        return m.n_edges if hasattr(m, 'n_edges') else int(m['edges'].shape[0])
+
+    def info(self):
+        return self._info
+
+    def edges(self):
+        m = self.merged
+        return m.edges() if hasattr(m, 'edges') and callable(m.edges) else m['edges']
+
+    def features(self):
+        m = self.merged
+        return m.features() if hasattr(m, 'features') and callable(m.features) else m['features']
+
+    def free(self):
+        if hasattr(self.merged, 'free'):
+            self.merged.free()
+
+
+def _exclusive_offset(n_local, group, device):
+    world = dist.get_world_size(group)
+    t = torch.tensor([n_local], dtype=torch.int64, device=device)
+    allc = [torch.empty_like(t) for _ in range(world)]
+    dist.all_gather(allc, t, group=group)
+    counts = [int(x.item()) for x in allc]
+    r = dist.get_rank(group)
+    return sum(counts[:r]), sum(counts)
+
+
+def rag_features_distributed(labels, data=None, offsets=None, own_begin=None, own_end=None,
+                             ignore_label=False, hist_range=(0.0, 1.0), group=None, backend=None):
+    """Global RAG + edge features of a z-slab-partitioned volume.
+
+    Every rank passes its slab (plus the halo plane below it, excluded via
+    ``own_begin``); the call is collective.  Returns a ``DistResult`` whose
+    edge rows are rows [edge_offset, edge_offset + n_edges) of the global
+    sorted edge table (same for nodes).
+    """
+    backend = backend or HipBackend()
+    world = dist.get_world_size(group)
+    keys, sums, recs, nodes, info = backend.local(labels, data, offsets, own_begin, own_end,
+                                                  ignore_label, hist_range)
+    dev = keys.device
+    n = keys.shape[0]
+    # splitters on u from an evenly spaced sample of the sorted local keys
+    if n > 0:
+        idx = torch.div(torch.arange(N_SAMPLES, device=dev, dtype=torch.int64) * n, N_SAMPLES,
+                        rounding_mode='floor')
+        samp = keys[:, 0].index_select(0, idx)
+    else:
+        samp = torch.zeros(N_SAMPLES, dtype=torch.int64, device=dev)
+    meta = torch.cat([samp, torch.tensor([n], dtype=torch.int64, device=dev)])
+    gathered = [torch.empty_like(meta) for _ in range(world)]
+    dist.all_gather(gathered, meta, group=group)
+    g = torch.stack(gathered).cpu().numpy()
+    splitters = weighted_splitters(g[:, :N_SAMPLES], g[:, N_SAMPLES], world)
+
+    # edge rows -> owner of u
+    rows = pack_rows(keys, sums, recs)
+    recv = exchange(rows, split_counts(keys[:, 0], splitters), group)
+    rk, rs, rr = unpack_rows(recv)
+    merged = backend.merge(rk, rs, rr, hist_range)
+    n_loc = merged.n_edges if hasattr(merged, 'n_edges') else int(merged['edges'].shape[0])
+
+    # nodes -> the same ranges
+    nrecv = exchange(nodes.reshape(-1), split_counts(nodes.reshape(-1), splitters), group)
+    node_shard = backend.unique(nrecv)
+
+    e_off, e_tot = _exclusive_offset(n_loc, group, dev)
+    n_off, n_tot = _exclusive_offset(int(node_shard.shape[0]), group, dev)
+    return DistResult(merged, node_shard, e_off, e_tot, n_off, n_tot, info)

@@ -36,6 +36,8 @@ from .blocking import blocking
 N_FEATURES = 10
 STATS_SUFFIX = '_stats'   # companion varlen dataset: per edge (sum, sumsq, 48 record words)
 STATS_WIDTH = 2 + rag.WIDE_WORDS
+ORD_POS_INF = 0xFF800000   # order-preserving u32 code of +inf (ctg_internal.h f2ord)
+ORD_NEG_INF = 0x007FFFFF   # ... of -inf
 
 
 def _open(path, mode='a'):
@@ -271,14 +273,20 @@ def _block_features(graphPath, subgraphKey, dataPath, dataKey, labelsPath, label
                     data = ds_data[(slice(0, len(offsets)),) + tuple(slice(b, e) for b, e in zip(rb, re_))]
                 own_b = [b - r for b, r in zip(block.begin, rb)]
                 own_e = [e - r for e, r in zip(block.end, rb)]
+                # affinities: keep every sampled pair; the block's sub-graph edge
+                # list is the adjacency filter (map_edge_ids below), as in ndist
                 res = rag.rag_features(labels, data, offsets=offsets, own_begin=own_b, own_end=own_e,
-                                       ignore_label=ignore, keep_stats=True)
+                                       ignore_label=ignore, keep_stats=True, no_adj_filter=offsets is not None)
                 rows = rag.map_edge_ids(res['edges'], edges_b) if res['edges'].shape[0] else \
                     np.full(edges_b.shape[0], -1, np.int64)
                 hit = rows >= 0
                 feats = np.zeros((edges_b.shape[0], N_FEATURES), np.float64)
                 sums = np.zeros((edges_b.shape[0], 2), np.float64)
                 recs = np.zeros((edges_b.shape[0], rag.WIDE_WORDS), np.uint32)
+                # edges of the sub-graph without owned samples: empty records
+                # (ordered +inf min / -inf max are the identities of the merge)
+                recs[:, 43] = ORD_POS_INF
+                recs[:, 44] = ORD_NEG_INF
                 feats[hit] = res['features'][rows[hit]]
                 sums[hit] = res['sums'][rows[hit]]
                 recs[hit] = res['records'][rows[hit]]

@@ -101,6 +101,15 @@ class Result:
         t = self._torch_copy((self.n_edges, 2), torch.int64, L.load().ctg_result_copy_edges)
         return t.view(torch.uint64) if hasattr(torch, 'uint64') else t
 
+    def nodes_torch(self):
+        import torch
+        return self._torch_copy((self.n_nodes,), torch.int64, L.load().ctg_result_copy_nodes)
+
+    def edges_torch_i64(self):
+        """(E,2) int64 view of the uint64 edge table (labels < 2^63)."""
+        import torch
+        return self._torch_copy((self.n_edges, 2), torch.int64, L.load().ctg_result_copy_edges)
+
     def features_torch(self):
         import torch
         return self._torch_copy((self.n_edges, N_FEATURES), torch.float64, L.load().ctg_result_copy_features)
@@ -129,13 +138,14 @@ def _check_offsets(offsets):
 
 
 def rag_features_handle(labels, data=None, offsets=None, own_begin=None, own_end=None, ignore_label=False,
-                        hist_range=(0.0, 1.0), keep_stats=False, stream=None):
+                        hist_range=(0.0, 1.0), keep_stats=False, stream=None, no_adj_filter=False):
     """Run the hot path and return the device-resident ``Result`` handle.
 
     labels: (Z,Y,X) uint64/uint32 numpy array or CUDA tensor (int64/int32 views
     of unsigned labels are accepted for torch); data: None, (Z,Y,X) boundary
     map or (C,Z,Y,X) affinities (float32 or uint8); offsets: C x 3 for
-    affinities.
+    affinities.  keep_stats keeps the mergeable wide records; no_adj_filter
+    (affinities) keeps sampled pairs that are not edges of this array's RAG.
     """
     lib = L.load()
     dev = L.init_device()
@@ -182,6 +192,7 @@ def rag_features_handle(labels, data=None, offsets=None, own_begin=None, own_end
     else:
         if tuple(data.shape) != tuple(shape):
             raise ValueError('boundary map shape %s != labels shape %s' % (tuple(data.shape), tuple(shape)))
+    flags = (L.CTG_KEEP_STATS if keep_stats else 0) | (L.CTG_NO_ADJ_FILTER if no_adj_filter else 0)
     sh = _shape_arr(shape)
     ob = _shape_arr(own_begin) if own_begin is not None else None
     oe = _shape_arr(own_end) if own_end is not None else None
@@ -190,16 +201,17 @@ def rag_features_handle(labels, data=None, offsets=None, own_begin=None, own_end
     h = ctypes.c_void_p()
     rc = lib.ctg_rag_features(_ptr(labels), label_bits, _ptr(data), kind, n_ch, off_ptr, sh, ob, oe,
                               int(bool(ignore_label)), float(hist_range[0]), float(hist_range[1]),
-                              int(bool(keep_stats)), L.CTG_MEM_DEVICE if on_dev else L.CTG_MEM_HOST,
+                              flags, L.CTG_MEM_DEVICE if on_dev else L.CTG_MEM_HOST,
                               stream, ctypes.byref(h))
     L.check(rc, 'ctg_rag_features')
     return Result(h, dev)
 
 
 def rag_features(labels, data=None, offsets=None, own_begin=None, own_end=None, ignore_label=False,
-                 hist_range=(0.0, 1.0), keep_stats=False):
+                 hist_range=(0.0, 1.0), keep_stats=False, no_adj_filter=False):
     """Host convenience: returns dict(edges, nodes, features[, sums, records])."""
-    r = rag_features_handle(labels, data, offsets, own_begin, own_end, ignore_label, hist_range, keep_stats)
+    r = rag_features_handle(labels, data, offsets, own_begin, own_end, ignore_label, hist_range, keep_stats,
+                            no_adj_filter=no_adj_filter)
     out = dict(edges=r.edges(), nodes=r.nodes())
     if data is not None:
         out['features'] = r.features()
@@ -231,20 +243,56 @@ def unique_labels(labels, begin=None, end=None):
     return nodes
 
 
-def merge_stats(keys, sums, records, hist_range=(0.0, 1.0), keep_stats=False):
-    """Combine partial statistics tables (wide records) -> dict(edges, features[, sums, records])."""
+def merge_stats_handle(keys, sums, records, hist_range=(0.0, 1.0), keep_stats=False, stream=None):
+    """Device-resident merge of partial statistics: keys (n,2), sums (n,2)
+    float64, records (n,48) 32-bit words; numpy (host) or CUDA tensors."""
     lib = L.load()
     dev = L.init_device()
-    keys = np.ascontiguousarray(np.asarray(keys, dtype=np.uint64).reshape(-1, 2))
-    sums = np.ascontiguousarray(np.asarray(sums, dtype=np.float64).reshape(-1, 2))
-    records = np.ascontiguousarray(np.asarray(records, dtype=np.uint32).reshape(-1, WIDE_WORDS))
-    n = keys.shape[0]
-    assert sums.shape[0] == n and records.shape[0] == n
+    on_dev = _is_torch(keys)
+    if on_dev:
+        for t in (keys, sums, records):
+            assert _is_torch(t) and t.is_cuda and t.is_contiguous(), 'merge inputs must be contiguous CUDA tensors'
+        n = keys.shape[0]
+        assert keys.element_size() == 8 and keys.numel() == 2 * n
+        assert sums.element_size() == 8 and sums.numel() == 2 * n
+        assert records.element_size() == 4 and records.numel() == WIDE_WORDS * n
+    else:
+        keys = np.ascontiguousarray(np.asarray(keys, dtype=np.uint64).reshape(-1, 2))
+        sums = np.ascontiguousarray(np.asarray(sums, dtype=np.float64).reshape(-1, 2))
+        records = np.ascontiguousarray(np.asarray(records, dtype=np.uint32).reshape(-1, WIDE_WORDS))
+        n = keys.shape[0]
+        assert sums.shape[0] == n and records.shape[0] == n
+    if stream is None:
+        stream = _current_stream(on_dev)
     h = ctypes.c_void_p()
     rc = lib.ctg_merge_stats(_ptr(keys), _ptr(sums), _ptr(records), n, float(hist_range[0]),
-                             float(hist_range[1]), int(bool(keep_stats)), L.CTG_MEM_HOST, None, ctypes.byref(h))
+                             float(hist_range[1]), int(bool(keep_stats)),
+                             L.CTG_MEM_DEVICE if on_dev else L.CTG_MEM_HOST, stream, ctypes.byref(h))
     L.check(rc, 'ctg_merge_stats')
-    r = Result(h, dev)
+    return Result(h, dev)
+
+
+def unique_values_handle(values, stream=None):
+    """Sorted unique values of a uint64 list (numpy or CUDA int64 tensor) -> Result (nodes)."""
+    lib = L.load()
+    dev = L.init_device()
+    on_dev = _is_torch(values)
+    if not on_dev:
+        values = np.ascontiguousarray(np.asarray(values, dtype=np.uint64).reshape(-1))
+    else:
+        assert values.is_cuda and values.is_contiguous() and values.element_size() == 8
+    if stream is None:
+        stream = _current_stream(on_dev)
+    h = ctypes.c_void_p()
+    L.check(lib.ctg_unique_values(_ptr(values), int(values.shape[0]),
+                                  L.CTG_MEM_DEVICE if on_dev else L.CTG_MEM_HOST, stream, ctypes.byref(h)),
+            'ctg_unique_values')
+    return Result(h, dev)
+
+
+def merge_stats(keys, sums, records, hist_range=(0.0, 1.0), keep_stats=False):
+    """Combine partial statistics tables (wide records) -> dict(edges, features[, sums, records])."""
+    r = merge_stats_handle(keys, sums, records, hist_range, keep_stats)
     out = dict(edges=r.edges(), features=r.features())
     if keep_stats:
         out['sums'], out['records'] = r.stats()

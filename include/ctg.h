@@ -53,6 +53,12 @@ extern "C" {
 #define CTG_DATA_F32 1
 #define CTG_DATA_U8 2     /* mapped to [0,1] by /255 before binning (SURVEY OPEN-7) */
 
+/* ctg_rag_features flags */
+#define CTG_KEEP_STATS 1      /* keep mergeable per-edge statistics (ctg_result_copy_stats) */
+#define CTG_NO_ADJ_FILTER 2   /* affinities: keep sample pairs that are not nearest-neighbour
+                                 edges of this array (their records carry no ADJ bit); the
+                                 caller filters after a merge or by an edge list */
+
 #define CTG_MAX_CHANNELS 24
 #define CTG_N_FEATURES 10
 #define CTG_NBINS 40
@@ -77,6 +83,7 @@ int ctg_device_count(int* count);
  *              own_begin is the lower-halo geometry of increaseRoi=True.
  *   ignore_label  drop edges that contain label 0 (nodes still contain 0)
  *   hist_lo/hi    histogram range (nifty: [0,1])
+ *   flags         CTG_KEEP_STATS | CTG_NO_ADJ_FILTER
  * Result: sorted unique edges (u<v, lexicographic), sorted unique nodes and,
  * if data != NULL, an (E,10) float64 feature table
  * [mean, var, min, q10, q25, q50, q75, q90, max, count].
@@ -86,12 +93,17 @@ int ctg_rag_features(const void* labels, int label_bits,
                      int n_channels, const int32_t* offsets,
                      const int64_t* shape, const int64_t* own_begin, const int64_t* own_end,
                      int ignore_label, double hist_lo, double hist_hi,
-                     int keep_stats, int mem, void* stream, ctg_result** out);
+                     int flags, int mem, void* stream, ctg_result** out);
 
 /* sorted unique labels of labels[begin:end] (box in array coordinates) */
 int ctg_unique_labels(const uint64_t* labels, const int64_t* shape,
                       const int64_t* begin, const int64_t* end,
                       int mem, void* stream, ctg_result** out);
+
+/* sorted unique values of an (n,) uint64 list -> result nodes (union of the
+ * per-slab node lists of the multi-GPU path; ndist.mergeSubgraphs node union,
+ * graph/merge_sub_graphs.py:130-135) */
+int ctg_unique_values(const uint64_t* values, int64_t n, int mem, void* stream, ctg_result** out);
 
 /* Combine partial statistics tables (wide records, one per (part, edge)) into
  * one table: counts add, sums add, min/max elementwise, histograms add.

@@ -40,24 +40,33 @@ N_FEATURES = 10  # mean, var, q0(min), q10, q25, q50, q75, q90, q100(max), count
 # faces
 # ----------------------------------------------------------------------------
 
-def _face_slices(shape, axis, own_begin):
+def _own_end(shape, own_end):
+    return tuple(shape) if own_end is None else tuple(min(int(e), int(s)) for e, s in zip(own_end, shape))
+
+
+def _face_slices(shape, axis, own_begin, own_end=None):
     """Slices (lower, upper) selecting every face (p, p+e_axis) whose upper
-    voxel q = p + e_axis lies in the owned box [own_begin, shape).
+    voxel q = p + e_axis lies in the owned box [own_begin, own_end).
 
     own_begin = (0,0,0) selects every face of the array (whole-volume RAG as in
     nifty.graph.rag.gridRag, test_graph.py:79,108).  A 1-voxel own_begin on an
-    axis is the "increaseRoi" halo geometry of initial_sub_graphs.py:124-129.
+    axis is the "increaseRoi" halo geometry of initial_sub_graphs.py:124-129;
+    own_end < shape is a block inside a larger (halo) array
+    (block_edge_features.py:189-211 geometry twin).
     """
+    end = _own_end(shape, own_end)
     up, lo = [], []
     for ax in range(3):
         b = own_begin[ax]
+        e = max(end[ax], b)
         if ax == axis:
             b = max(b, 1)
-            up.append(slice(b, shape[ax]))
-            lo.append(slice(b - 1, shape[ax] - 1))
+            e = max(e, b)
+            up.append(slice(b, e))
+            lo.append(slice(b - 1, e - 1))
         else:
-            up.append(slice(b, shape[ax]))
-            lo.append(slice(b, shape[ax]))
+            up.append(slice(b, e))
+            lo.append(slice(b, e))
     return tuple(lo), tuple(up)
 
 
@@ -86,7 +95,7 @@ def _unique_pairs(uv, return_inverse=False):
     return uniq, inv
 
 
-def face_keys(labels, own_begin=(0, 0, 0), ignore_label=False):
+def face_keys(labels, own_begin=(0, 0, 0), ignore_label=False, own_end=None):
     """All boundary faces as canonical (u<v) keys, per axis.
 
     Returns list of (key_uv (n,2), lower_index_slices, upper_index_slices, mask).
@@ -95,7 +104,7 @@ def face_keys(labels, own_begin=(0, 0, 0), ignore_label=False):
     assert labels.ndim == 3
     out = []
     for axis in range(3):
-        lo, up = _face_slices(labels.shape, axis, own_begin)
+        lo, up = _face_slices(labels.shape, axis, own_begin, own_end)
         a = labels[lo]
         b = labels[up]
         mask = a != b
@@ -111,14 +120,14 @@ def face_keys(labels, own_begin=(0, 0, 0), ignore_label=False):
 # graph
 # ----------------------------------------------------------------------------
 
-def rag_edges(labels, own_begin=(0, 0, 0), ignore_label=False):
+def rag_edges(labels, own_begin=(0, 0, 0), ignore_label=False, own_end=None):
     """Sorted unique (u<v) label pairs over forward faces.
 
     Equals ``nrag.gridRag(seg).uvIds()`` (test_graph.py:79-84, 108-115) for
     own_begin = 0 and ignore_label False.  With ``ignore_label`` every edge that
     contains label 0 is dropped (initial_sub_graphs.py:38-43,147 config key).
     """
-    parts = [k for k, _, _, _ in face_keys(labels, own_begin, ignore_label)]
+    parts = [k for k, _, _, _ in face_keys(labels, own_begin, ignore_label, own_end)]
     uv = np.concatenate(parts, axis=0) if parts else np.zeros((0, 2), np.uint64)
     return _unique_pairs(uv)
 
@@ -326,8 +335,16 @@ def finalize_features(stats, lo, hi, nbins=NBINS):
     return out
 
 
+def as_samples(data):
+    """uint8 maps are sampled as value/255 in float32 (SURVEY OPEN-7 default)."""
+    data = np.asarray(data)
+    if data.dtype == np.uint8:
+        return data.astype(np.float32) / np.float32(255.0)
+    return data.astype(np.float32, copy=False)
+
+
 def boundary_features(labels, data, own_begin=(0, 0, 0), ignore_label=False,
-                      lo=0.0, hi=1.0, nbins=NBINS, return_stats=False):
+                      lo=0.0, hi=1.0, nbins=NBINS, return_stats=False, own_end=None):
     """RAG + boundary-map edge features, whole-volume semantics.
 
     Every boundary face (p, q=p+e_a) whose upper voxel lies in the owned box
@@ -337,10 +354,10 @@ def boundary_features(labels, data, own_begin=(0, 0, 0), ignore_label=False,
     Returns (edges (E,2) uint64, features (E,10) float64).
     """
     labels = np.asarray(labels)
-    data = np.asarray(data)
+    data = as_samples(data)
     assert data.shape == labels.shape
     keys, vals = [], []
-    for uv, lo_sl, up_sl, mask in face_keys(labels, own_begin, ignore_label):
+    for uv, lo_sl, up_sl, mask in face_keys(labels, own_begin, ignore_label, own_end):
         a = data[lo_sl][mask]
         b = data[up_sl][mask]
         keys.append(uv)
@@ -358,21 +375,27 @@ def boundary_features(labels, data, own_begin=(0, 0, 0), ignore_label=False,
 
 
 def affinity_features(labels, affs, offsets, own_begin=(0, 0, 0), ignore_label=False,
-                      lo=0.0, hi=1.0, nbins=NBINS, return_stats=False):
+                      lo=0.0, hi=1.0, nbins=NBINS, return_stats=False, own_end=None, edge_list=None):
     """RAG + affinity-map edge features.
 
     affs is channel-first (C,Z,Y,X) (block_edge_features.py:136,215).  For
     channel c with offset o_c and voxel p in the owned box, q = p + o_c inside
     the array: if L[p] != L[q] and (min,max) is an edge of the RAG (faces with
     upper voxel in the owned box), sample affs[c, p].  Pairs that are not RAG
-    edges (long-range, non-adjacent) are skipped.
+    edges (long-range, non-adjacent) are skipped.  With ``edge_list`` (a
+    block's sub-graph edges, the ndist per-block call) the output rows are
+    that list and it is the adjacency filter.
     """
     labels = np.asarray(labels)
-    affs = np.asarray(affs)
+    affs = as_samples(affs)
     assert affs.ndim == 4 and affs.shape[1:] == labels.shape
     assert affs.shape[0] == len(offsets)
-    edges = rag_edges(labels, own_begin, ignore_label)
+    if edge_list is None:
+        edges = rag_edges(labels, own_begin, ignore_label, own_end)
+    else:
+        edges = _unique_pairs(np.asarray(edge_list, dtype=np.uint64).reshape(-1, 2))
     shape = labels.shape
+    end = _own_end(shape, own_end)
     keys, vals = [], []
     for c, off in enumerate(offsets):
         psl, qsl = [], []
@@ -380,7 +403,7 @@ def affinity_features(labels, affs, offsets, own_begin=(0, 0, 0), ignore_label=F
             o = int(off[ax])
             b = own_begin[ax]
             p0 = max(b, -o)
-            p1 = min(shape[ax], shape[ax] - o)
+            p1 = min(end[ax], shape[ax] - o)
             if p1 <= p0:
                 p0 = p1 = 0
             psl.append(slice(p0, p1))

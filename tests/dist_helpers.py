@@ -1,0 +1,77 @@
+"""Oracle-backed stand-in for dist.HipBackend, used by the gloo (CPU) tests of
+the multi-GPU exchange logic.  Test infrastructure: it wraps oracle/ and the
+wide-record layout of include/ctg.h (42 histogram slots, cnt|ADJ, ordered
+min, ordered max, pad) so that the partition / all_to_all / merge code of
+cluster_tools_amd/dist.py runs unchanged on CPU tensors.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from oracle import rag_oracle as O
+
+WIDE = 48
+ADJ = np.uint32(0x80000000)
+
+
+def f2ord(x):
+    b = np.asarray(x, dtype=np.float32).view(np.uint32)
+    return np.where(b & np.uint32(0x80000000), ~b, b | np.uint32(0x80000000)).astype(np.uint32)
+
+
+def ord2f(o):
+    o = np.asarray(o, dtype=np.uint32)
+    b = np.where(o & np.uint32(0x80000000), o & np.uint32(0x7FFFFFFF), ~o).astype(np.uint32)
+    return b.view(np.float32)
+
+
+def encode_stats(stats):
+    """oracle _accumulate stats -> (sums (E,2) f64, records (E,48) u32)."""
+    c = stats['count'].astype(np.float64)
+    n = c.shape[0]
+    sums = np.zeros((n, 2))
+    sums[:, 0] = stats['sum']
+    with np.errstate(invalid='ignore', divide='ignore'):
+        sums[:, 1] = stats['m2'] + np.where(c > 0, stats['sum'] ** 2 / np.maximum(c, 1), 0.0)
+    rec = np.zeros((n, WIDE), dtype=np.uint32)
+    rec[:, :O.NBINS + 2] = stats['hist'].astype(np.uint32)
+    rec[:, 42] = stats['count'].astype(np.uint32) | ADJ
+    rec[:, 43] = f2ord(stats['min'])
+    rec[:, 44] = f2ord(stats['max'])
+    return sums, rec
+
+
+def decode_stats(sums, rec):
+    c = (rec[:, 42] & np.uint32(0x7FFFFFFF)).astype(np.int64)
+    s = sums[:, 0]
+    with np.errstate(invalid='ignore', divide='ignore'):
+        mean = np.where(c > 0, s / np.maximum(c, 1), 0.0)
+    m2 = sums[:, 1] - np.where(c > 0, s * s / np.maximum(c, 1), 0.0)
+    return dict(count=c, sum=s, mean=mean, m2=m2,
+                min=ord2f(rec[:, 43]).astype(np.float64), max=ord2f(rec[:, 44]).astype(np.float64),
+                hist=rec[:, :O.NBINS + 2].astype(np.int64))
+
+
+class OracleBackend:
+    def local(self, labels, data, offsets, own_begin, own_end, ignore_label, hist_range):
+        lab = np.asarray(labels)
+        edges, _, stats = O.boundary_features(lab, np.asarray(data), own_begin=own_begin,
+                                              ignore_label=ignore_label, lo=hist_range[0], hi=hist_range[1],
+                                              return_stats=True)
+        sums, rec = encode_stats(stats)
+        nodes = np.unique(edges.reshape(-1))
+        return (torch.from_numpy(edges.astype(np.int64)), torch.from_numpy(sums),
+                torch.from_numpy(rec.view(np.int32)), torch.from_numpy(nodes.astype(np.int64)), (0, 0))
+
+    def merge(self, keys, sums, recs, hist_range):
+        k = keys.numpy().astype(np.uint64)
+        if k.shape[0] == 0:
+            return dict(edges=np.zeros((0, 2), np.uint64), features=np.zeros((0, O.N_FEATURES)))
+        edges, inv = O._unique_pairs(k, return_inverse=True)
+        st = decode_stats(sums.numpy(), recs.numpy().view(np.uint32))
+        merged = O.merge_feature_stats([(inv, st)], edges.shape[0], hist_range[0], hist_range[1])
+        return dict(edges=edges, features=O.finalize_features(merged, hist_range[0], hist_range[1]))
+
+    def unique(self, values):
+        return torch.from_numpy(np.unique(values.numpy()))

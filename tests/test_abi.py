@@ -1,0 +1,70 @@
+"""The C-ABI library loads and exports every symbol include/ctg.h declares
+(CPU: no compute calls); the Python shim binds exactly those symbols; the
+product path has no CPU fallback."""
+import ctypes
+import os
+import re
+
+import pytest
+
+from cluster_tools_amd import _lib
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_functions():
+    with open(os.path.join(ROOT, 'include', 'ctg.h')) as fh:
+        src = fh.read()
+    src = re.sub(r'/\*.*?\*/', '', src, flags=re.S)
+    return sorted(set(re.findall(r'\b(ctg_\w+)\s*\(', src)))
+
+
+def header_defines():
+    with open(os.path.join(ROOT, 'include', 'ctg.h')) as fh:
+        return dict(re.findall(r'#define\s+(CTG_\w+)\s+(-?\d+)', fh.read()))
+
+
+def test_header_parses():
+    fns = header_functions()
+    assert 'ctg_rag_features' in fns and 'ctg_free' in fns and len(fns) >= 20
+
+
+def test_library_exports_every_header_symbol():
+    lib = ctypes.CDLL(_lib.LIB_PATH)
+    missing = [f for f in header_functions() if not hasattr(lib, f)]
+    assert not missing, missing
+
+
+def test_shim_binds_exactly_the_header():
+    assert sorted(_lib.PROTOTYPES) == header_functions()
+
+
+def test_shim_constants_match_header():
+    d = header_defines()
+    for name, val in d.items():
+        if hasattr(_lib, name):
+            assert getattr(_lib, name) == int(val), name
+    for name in ('CTG_KEEP_STATS', 'CTG_NO_ADJ_FILTER', 'CTG_MEM_DEVICE', 'CTG_DATA_U8',
+                 'CTG_WIDE_RECORD_WORDS', 'CTG_MAX_CHANNELS'):
+        assert getattr(_lib, name) == int(d[name]), name
+
+
+def test_version_without_gpu():
+    assert _lib.load().ctg_version() >= 1
+
+
+def test_missing_library_fails_loudly(monkeypatch, tmp_path):
+    monkeypatch.setattr(_lib, '_lib', None)
+    monkeypatch.setattr(_lib, 'LIB_PATH', str(tmp_path / 'libctg.so'))
+    with pytest.raises(_lib.CtgError):
+        _lib.load()
+
+
+def test_product_package_does_not_import_oracle():
+    pkg = os.path.join(ROOT, 'cluster_tools_amd')
+    for dirpath, _, files in os.walk(pkg):
+        for f in files:
+            if f.endswith('.py'):
+                with open(os.path.join(dirpath, f)) as fh:
+                    src = fh.read()
+                assert not re.search(r'^\s*(from|import)\s+oracle\b', src, re.M), f

@@ -1,0 +1,114 @@
+"""Multi-rank logic of cluster_tools_amd/dist.py on CPU (gloo, world_size 2 and 3).
+
+Each rank holds one z-slab (+ the halo plane below it) of a synthetic volume,
+builds its partial table with the oracle-backed backend, and the real
+partition / all_to_all / merge code of dist.py produces the rank shards.
+Their concatenation must equal the whole-volume oracle: bit-exact edges and
+nodes, features within 1e-9 (same float64 statistics, merged by Chan's rule).
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from cluster_tools_amd import dist as cdist
+from cluster_tools_amd import synthetic
+from oracle import rag_oracle as O
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, shape, cell, outdir, ignore_label):
+    import torch.distributed as dist
+    from tests.dist_helpers import OracleBackend
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    lab, bnd = synthetic.generate(shape, cell=cell, seed=3)
+    Z = shape[0]
+    z0 = [Z * r // world for r in range(world + 1)]
+    halo = 1 if rank > 0 else 0
+    sl = slice(z0[rank] - halo, z0[rank + 1])
+    res = cdist.rag_features_distributed(np.ascontiguousarray(lab[sl]), np.ascontiguousarray(bnd[sl]),
+                                         own_begin=(halo, 0, 0), ignore_label=ignore_label,
+                                         backend=OracleBackend())
+    np.save(os.path.join(outdir, 'e%d.npy' % rank), np.asarray(res.edges()))
+    np.save(os.path.join(outdir, 'f%d.npy' % rank), np.asarray(res.features()))
+    np.save(os.path.join(outdir, 'n%d.npy' % rank), res.node_shard.numpy())
+    np.save(os.path.join(outdir, 'o%d.npy' % rank),
+            np.array([res.edge_offset, res.n_edges_global, res.node_offset, res.n_nodes_global]))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize('world,shape,cell,ignore', [
+    (2, (24, 40, 36), 6, False),
+    (3, (30, 33, 29), 5, True),
+])
+def test_distributed_matches_whole_volume(tmp_path, world, shape, cell, ignore):
+    mp.spawn(_worker, args=(world, _free_port(), shape, cell, str(tmp_path), ignore), nprocs=world, join=True)
+    lab, bnd = synthetic.generate(shape, cell=cell, seed=3)
+    e_ref, f_ref = O.boundary_features(lab, bnd, ignore_label=ignore)
+    nodes_ref = O.unique_labels(O.rag_edges(lab))  # endpoints of the unfiltered RAG
+    es = [np.load(tmp_path / ('e%d.npy' % r)) for r in range(world)]
+    fs = [np.load(tmp_path / ('f%d.npy' % r)) for r in range(world)]
+    ns = [np.load(tmp_path / ('n%d.npy' % r)) for r in range(world)]
+    offs = [np.load(tmp_path / ('o%d.npy' % r)) for r in range(world)]
+    e = np.concatenate(es).astype(np.uint64)
+    f = np.concatenate(fs)
+    n = np.concatenate(ns).astype(np.uint64)
+    np.testing.assert_array_equal(e, e_ref)
+    np.testing.assert_allclose(f, f_ref, rtol=1e-9, atol=1e-12)
+    np.testing.assert_array_equal(n, nodes_ref)
+    # offsets are the exclusive prefix of the shard sizes, totals agree
+    acc_e = acc_n = 0
+    for r in range(world):
+        assert offs[r][0] == acc_e and offs[r][2] == acc_n
+        acc_e += len(es[r])
+        acc_n += len(ns[r])
+        assert offs[r][1] == e_ref.shape[0] and offs[r][3] == nodes_ref.shape[0]
+    # every shard is non-empty for these sizes (splitters balance the ranks)
+    assert all(len(x) > 0 for x in es)
+
+
+def test_weighted_splitters_balance():
+    rng = np.random.default_rng(0)
+    keys = [np.sort(rng.integers(r * 1000, r * 1000 + 1500, size=n)) for r, n in enumerate([5000, 100, 9000])]
+    S = 64
+    samples = np.stack([k[(np.arange(S) * len(k)) // S] for k in keys])
+    sp = cdist.weighted_splitters(samples, [len(k) for k in keys], 3)
+    assert sp.shape == (2,) and sp[0] <= sp[1]
+    allk = np.sort(np.concatenate(keys))
+    owner = np.searchsorted(sp, allk, side='right')
+    frac = np.bincount(owner, minlength=3) / allk.size
+    assert np.all(np.abs(frac - 1 / 3) < 0.05)
+
+
+def test_weighted_splitters_empty_ranks():
+    sp = cdist.weighted_splitters(np.zeros((4, 8), np.int64), [0, 0, 0, 0], 4)
+    assert sp.shape == (3,)
+    sp = cdist.weighted_splitters(np.array([[5] * 8, [0] * 8]), [10, 0], 2)
+    assert list(sp) == [5]
+
+
+def test_split_counts_and_rows_roundtrip():
+    k = torch.tensor([1, 1, 2, 5, 5, 5, 9], dtype=torch.int64)
+    assert cdist.split_counts(k, np.array([2, 6])) == [2, 4, 1]
+    assert cdist.split_counts(k, np.array([0, 100])) == [0, 7, 0]
+    assert cdist.split_counts(k, np.array([], np.int64)) == [7]
+    n = 5
+    keys = torch.arange(2 * n, dtype=torch.int64).reshape(n, 2)
+    sums = torch.rand(n, 2, dtype=torch.float64)
+    recs = torch.randint(-2 ** 31, 2 ** 31 - 1, (n, 48), dtype=torch.int32)
+    rows = cdist.pack_rows(keys, sums, recs)
+    assert rows.shape == (n, cdist.ROW_WORDS)
+    k2, s2, r2 = cdist.unpack_rows(rows)
+    assert torch.equal(k2, keys) and torch.equal(s2, sums) and torch.equal(r2, recs)

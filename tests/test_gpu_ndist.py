@@ -1,0 +1,161 @@
+"""The nifty.distributed mirror end to end on N5 containers (GPU).
+
+Re-expresses the reference's hot-path tests without CREMI data, nifty or
+luigi: the job bodies' call sequence of graph/initial_sub_graphs.py,
+merge_sub_graphs.py, map_edge_ids.py, features/block_edge_features.py and
+merge_edge_features.py, with the assertions of test/graph/test_graph.py:27-115
+(per block and whole volume) and test/features/test_edge_features.py:32-77
+(whole-volume features), checked against the oracle.
+"""
+import numpy as np
+import pytest
+
+from cluster_tools_amd import n5, ndist
+from cluster_tools_amd import synthetic as S
+from cluster_tools_amd.blocking import blocking
+from oracle import rag_oracle as O
+
+from test_gpu_parity import check_features
+
+pytestmark = pytest.mark.gpu
+
+SHAPE = (24, 40, 36)
+BLOCK = (8, 16, 16)
+
+
+def _setup(tmp_path, lab, data=None, ignore_label=False):
+    p = str(tmp_path / 'data.n5')
+    with n5.File(p) as f:
+        f.create_dataset('seg', data=lab, chunks=BLOCK, compression='gzip')
+        if data is not None:
+            ch = BLOCK if data.ndim == 3 else (1,) + BLOCK
+            f.create_dataset('bnd', data=data, chunks=ch, compression='gzip')
+        # initial_sub_graphs.py:64-75 (the task creates the datasets)
+        g = f.require_group('s0/sub_graphs')
+        g.attrs['shape'] = list(lab.shape)
+        g.attrs['ignore_label'] = bool(ignore_label)
+        for k in ('nodes', 'edges', 'edge_ids'):
+            g.require_dataset(k, shape=lab.shape, chunks=BLOCK, dtype='uint64', compression='gzip')
+    return p
+
+
+def _graph(p, ignore_label):
+    blk = blocking([0, 0, 0], list(SHAPE), list(BLOCK))
+    ids = list(range(blk.numberOfBlocks))
+    for b in ids:
+        bb = blk.getBlock(b)
+        ndist.computeMergeableRegionGraph(p, 'seg', bb.begin, bb.end, p, 's0/sub_graphs', ignore_label,
+                                          increaseRoi=True, serializeToVarlen=True)
+    ndist.mergeSubgraphs(p, subgraphKey='s0/sub_graphs', blockIds=ids, outKey='graph', numberOfThreads=4,
+                         serializeToVarlen=False)
+    ndist.mapEdgeIds(p, 'graph', subgraphKey='s0/sub_graphs', blockIds=ids, numberOfThreads=4)
+    return blk, ids
+
+
+@pytest.mark.parametrize('ignore_label', [False, True])
+def test_graph_workflow(gpu, tmp_path, ignore_label):
+    lab, _ = S.generate(SHAPE, cell=5, seed=31, with_boundary=False)
+    if ignore_label:
+        lab = np.where(lab % 7 == 0, 0, lab).astype(np.uint64)
+    p = _setup(tmp_path, lab, ignore_label=ignore_label)
+    blk, ids = _graph(p, ignore_label)
+    full = ndist.Graph(p, 'graph')
+    with n5.File(p, 'r') as f:
+        g = f['s0/sub_graphs']
+        for b in ids:
+            bb = blk.getBlock(b)
+            pos = blk.blockGridPosition(b)
+            inner = tuple(slice(x, y) for x, y in zip(bb.begin, bb.end))
+            outer = tuple(slice(max(x - 1, 0), y) for x, y in zip(bb.begin, bb.end))
+            nodes = g['nodes'].read_chunk(pos)
+            np.testing.assert_array_equal(nodes, np.unique(lab[inner]))                  # test_graph.py:53-60
+            edges = g['edges'].read_chunk(pos)
+            ref = O.rag_edges(lab[outer], ignore_label=ignore_label)
+            if edges is None:                                                              # :63-66
+                assert ref.shape[0] == 0
+                continue
+            edges = edges.reshape(-1, 2)
+            np.testing.assert_array_equal(edges, ref)                                     # :79-84
+            if not ignore_label:
+                np.testing.assert_array_equal(ndist.Graph(edges).nodes(), np.unique(lab[outer]))  # :70-77
+            np.testing.assert_array_equal(g['edge_ids'].read_chunk(pos).astype(np.int64),
+                                          full.findEdges(edges))                          # :89-93
+        gr = f['graph']
+        assert gr.attrs['numberOfEdges'] == full.numberOfEdges
+    ref = O.rag_edges(lab, ignore_label=ignore_label)                                       # :95-115
+    np.testing.assert_array_equal(full.uvIds(), ref)
+    assert full.numberOfNodes == len(np.unique(lab))
+    assert full.numberOfEdges == ref.shape[0]
+
+
+def _features(p, ids, E, fn, *extra, **kw):
+    with n5.File(p) as f:
+        ds = f.require_dataset('s0/sub_features', shape=SHAPE, chunks=BLOCK, dtype='float64', compression='gzip')
+        ds.attrs['n_features'] = 10
+        f.require_dataset('features', shape=(E, 10), chunks=(min(262144, E), 1), dtype='float64',
+                          compression='gzip')
+    fn(p, 's0/sub_graphs', p, 'bnd', p, 'seg', ids, p, 's0/sub_features', *extra, **kw)
+    # merge_edge_features.py:134-147: two jobs over edge-id ranges
+    half = E // 2
+    for b, e in ((0, half), (half, E)):
+        ndist.mergeFeatureBlocks(p, 's0/sub_graphs', p, 's0/sub_features', p, 'features', blockIds=ids,
+                                 edgeIdBegin=b, edgeIdEnd=e, numberOfThreads=2)
+    with n5.File(p, 'r') as f:
+        return f['features'][:]
+
+
+@pytest.mark.parametrize('dtype', ['float32', 'uint8'])
+def test_boundary_feature_workflow(gpu, tmp_path, dtype):
+    lab, bnd = S.generate(SHAPE, cell=5, seed=32)
+    data = bnd if dtype == 'float32' else np.round(bnd * 255).astype(np.uint8)
+    p = _setup(tmp_path, lab, data)
+    blk, ids = _graph(p, False)
+    E = ndist.Graph(p, 'graph').numberOfEdges
+    fn = (ndist.extractBlockFeaturesFromBoundaryMaps_float32 if dtype == 'float32'
+          else ndist.extractBlockFeaturesFromBoundaryMaps_uint8)
+    feats = _features(p, ids, E, fn, increaseRoi=True)
+    e_ref, f_ref = O.boundary_features(lab, data)        # whole volume (test_edge_features.py:32-77)
+    np.testing.assert_array_equal(ndist.Graph(p, 'graph').uvIds(), e_ref)
+    check_features(feats, f_ref)
+
+
+@pytest.mark.parametrize('offsets', [S.NN_OFFSETS, S.LR_OFFSETS])
+def test_affinity_feature_workflow(gpu, tmp_path, offsets):
+    lab, bnd = S.generate(SHAPE, cell=5, seed=33)
+    affs = S.affinities_from_boundary(bnd, offsets)
+    p = _setup(tmp_path, lab, affs)
+    blk, ids = _graph(p, False)
+    graph = ndist.Graph(p, 'graph')
+    E = graph.numberOfEdges
+    feats = _features(p, ids, E, ndist.extractBlockFeaturesFromAffinityMaps_float32, offsets)
+    # oracle: per block, samples owned by the block and filtered by the
+    # block's sub-graph (the ndist per-block semantics), merged over blocks
+    off = np.asarray(offsets)
+    halo_lo = [max(1, int(max(0, -off[:, a].min()))) for a in range(3)]
+    halo_hi = [int(max(0, off[:, a].max())) for a in range(3)]
+    parts = []
+    with n5.File(p, 'r') as f:
+        g = f['s0/sub_graphs']
+        for b in ids:
+            bb = blk.getBlock(b)
+            pos = blk.blockGridPosition(b)
+            eb = g['edges'].read_chunk(pos)
+            if eb is None:
+                continue
+            eb = eb.reshape(-1, 2)
+            rb = [max(x - h, 0) for x, h in zip(bb.begin, halo_lo)]
+            re_ = [min(y + h, s) for y, h, s in zip(bb.end, halo_hi, SHAPE)]
+            sl = tuple(slice(x, y) for x, y in zip(rb, re_))
+            own_b = [x - r for x, r in zip(bb.begin, rb)]
+            own_e = [y - r for y, r in zip(bb.end, rb)]
+            e_b, _, st = O.affinity_features(lab[sl], affs[(slice(None),) + sl], offsets, own_begin=own_b,
+                                             own_end=own_e, edge_list=eb, return_stats=True)
+            parts.append((graph.findEdges(e_b), st))
+    m = O.merge_feature_stats(parts, E)
+    f_ref = O.finalize_features(m, 0.0, 1.0)
+    check_features(feats, f_ref)
+    if offsets == S.NN_OFFSETS:
+        # nearest-neighbour offsets: every sample pair is adjacent and inside the
+        # halo'd block, so the block path equals the whole-volume definition
+        _, f_whole = O.affinity_features(lab, affs, offsets)
+        check_features(feats, f_whole)

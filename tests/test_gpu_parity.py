@@ -1,13 +1,18 @@
-"""GPU parity: the HIP path (libctg.so) against the CPU oracle.
+"""GPU parity: the HIP path (libctg.so, through the C ABI) against the oracle
+and the committed golden fixtures.
 
-Graph outputs must be bit-exact; mean/var/min/max within 1e-5 relative
-(north_star); quantiles within one histogram bin width (1/40 on [0,1]).
+Bars (north_star): graph outputs (edges, nodes, counts) bit-exact; mean, var,
+min, max within 1e-5 relative; quantiles within one histogram bin width
+(1/40 on [0,1]).
 """
+import json
+import os
+
 import numpy as np
 import pytest
 
-from cluster_tools_amd import synthetic as S
 from cluster_tools_amd import rag
+from cluster_tools_amd import synthetic as S
 from oracle import rag_oracle as O
 
 pytestmark = pytest.mark.gpu
@@ -15,6 +20,7 @@ pytestmark = pytest.mark.gpu
 RTOL = 1e-5
 ATOL = 1e-9
 BIN = 1.0 / 40
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'golden')
 
 
 def check_features(f_gpu, f_ref):
@@ -25,7 +31,118 @@ def check_features(f_gpu, f_ref):
     np.testing.assert_array_less(np.abs(f_gpu[:, 3:8] - f_ref[:, 3:8]), BIN + 1e-12)
 
 
-@pytest.mark.parametrize("shape,cell", [((32, 48, 70), 6), ((40, 64, 64), 10), ((17, 130, 65), 5)])
+@pytest.fixture(scope='module')
+def vol():
+    return dict(np.load(os.path.join(GOLD, 'volumes.npz')))
+
+
+@pytest.fixture(scope='module')
+def kats():
+    with open(os.path.join(GOLD, 'kats.json')) as fh:
+        return {k['name']: k for k in json.load(fh)}
+
+
+# ------------------------------------------------------------------ KATs
+@pytest.mark.parametrize('name', ['kat1_sample_rule', 'kat3_halo_plane', 'kat7_outliers'])
+def test_kat_boundary(gpu, kats, name):
+    k = kats[name]
+    out = rag.rag_features(np.asarray(k['labels'], np.uint64), np.asarray(k['data'], np.float32))
+    np.testing.assert_array_equal(out['edges'], np.asarray(k['edges'], np.uint64))
+    f = out['features']
+    np.testing.assert_array_equal(f[:, 9], k['count'])
+    np.testing.assert_allclose(f[:, 0], k['mean'], rtol=1e-12)
+    np.testing.assert_allclose(f[:, 2], k['min'], rtol=0)
+    np.testing.assert_allclose(f[:, 8], k['max'], rtol=0)
+    if 'var' in k:
+        np.testing.assert_allclose(f[:, 1], k['var'], rtol=1e-9, atol=1e-15)
+
+
+def test_kat_affinity(gpu, kats):
+    k = kats['kat6_affinity']
+    out = rag.rag_features(np.asarray(k['labels'], np.uint64), np.asarray(k['affs'], np.float32),
+                           offsets=k['offsets'])
+    np.testing.assert_array_equal(out['edges'], np.asarray(k['edges'], np.uint64))
+    np.testing.assert_array_equal(out['features'][:, 9], k['count'])
+    np.testing.assert_allclose(out['features'][:, 0], k['mean'], rtol=0)
+
+
+def test_kat_ignore_label_and_halo_graph(gpu, kats):
+    k = kats['kat4_ignore_label']
+    out = rag.rag_features(np.asarray(k['labels'], np.uint64), ignore_label=True)
+    np.testing.assert_array_equal(out['edges'], np.asarray(k['edges'], np.uint64))
+    np.testing.assert_array_equal(out['nodes'], k['nodes'])
+    k = kats['kat2_halo']
+    L = np.asarray(k['labels'], np.uint64)
+    # block 1 of KAT-2: ROI z in [1,4), owned faces = all of the ROI
+    out = rag.rag_features(L[1:])
+    np.testing.assert_array_equal(out['edges'], np.asarray(k['blocks'][1]['edges'], np.uint64))
+    np.testing.assert_array_equal(rag.unique_labels(L, (2, 0, 0), (4, 1, 1)), k['blocks'][1]['nodes'])
+    # block 0: one inner label, no edges
+    out = rag.rag_features(L[:2])
+    assert out['edges'].shape == (0, 2)
+    np.testing.assert_array_equal(out['nodes'], [1])
+
+
+# ------------------------------------------------------------- fixtures
+def test_golden_boundary_f32(gpu, vol):
+    out = rag.rag_features(vol['bf_labels'], vol['bf_data'])
+    np.testing.assert_array_equal(out['edges'], vol['bf_edges'])
+    np.testing.assert_array_equal(out['nodes'], vol['bf_nodes'])
+    check_features(out['features'], vol['bf_feats'])
+
+
+def test_golden_boundary_u8(gpu, vol):
+    out = rag.rag_features(vol['bf_labels'], vol['bu_data'])
+    np.testing.assert_array_equal(out['edges'], vol['bu_edges'])
+    check_features(out['features'], vol['bu_feats'])
+
+
+def test_golden_ignore_label(gpu, vol):
+    out = rag.rag_features(vol['ig_labels'], vol['bf_data'], ignore_label=True)
+    np.testing.assert_array_equal(out['edges'], vol['ig_edges'])
+    np.testing.assert_array_equal(out['nodes'], vol['ig_nodes'])   # nodes keep 0 (OPEN-2)
+    check_features(out['features'], vol['ig_feats'])
+
+
+def test_golden_owned_box(gpu, vol):
+    out = rag.rag_features(vol['bf_labels'], vol['bf_data'], own_begin=tuple(vol['ob_begin']),
+                           own_end=tuple(vol['ob_end']))
+    np.testing.assert_array_equal(out['edges'], vol['ob_edges'])
+    check_features(out['features'], vol['ob_feats'])
+
+
+def test_golden_affinity_nn(gpu, vol):
+    out = rag.rag_features(vol['bf_labels'], vol['nn_affs'], offsets=vol['nn_offsets'])
+    np.testing.assert_array_equal(out['edges'], vol['nn_edges'])
+    check_features(out['features'], vol['nn_feats'])
+
+
+def test_golden_affinity_long_range(gpu, vol):
+    lab, bnd = S.generate((10, 32, 32), cell=4, seed=5)
+    affs = S.affinities_from_boundary(bnd, vol['lr_offsets'])
+    out = rag.rag_features(lab, affs, offsets=vol['lr_offsets'])
+    np.testing.assert_array_equal(out['edges'], vol['lr_edges'])
+    check_features(out['features'], vol['lr_feats'])
+
+
+def test_golden_block_subgraphs(gpu, vol):
+    lab = vol['bf_labels']
+    blocks = O.blocking_blocks(lab.shape, tuple(vol['blk_shape']))
+    no = np.concatenate([[0], np.cumsum(vol['blk_nodes_len'])])
+    eo = np.concatenate([[0], np.cumsum(vol['blk_edges_len'])])
+    for i, (_, b, e) in enumerate(blocks):
+        roi = [max(x - 1, 0) for x in b]
+        sub = np.ascontiguousarray(lab[tuple(slice(r, y) for r, y in zip(roi, e))])
+        out = rag.rag_features(sub)
+        np.testing.assert_array_equal(out['edges'], vol['blk_edges'][eo[i]:eo[i + 1]])
+        inner_b = [x - r for x, r in zip(b, roi)]
+        inner_e = [y - r for y, r in zip(e, roi)]
+        np.testing.assert_array_equal(rag.unique_labels(sub, inner_b, inner_e), vol['blk_nodes'][no[i]:no[i + 1]])
+
+
+# --------------------------------------------------------- random volumes
+@pytest.mark.parametrize("shape,cell", [((32, 48, 70), 6), ((40, 64, 64), 10), ((17, 130, 65), 5),
+                                        ((3, 5, 200), 3), ((70, 2, 1), 2)])
 def test_boundary_whole_volume(gpu, shape, cell):
     lab, bnd = S.generate(shape, cell=cell, seed=3)
     e_ref, f_ref = O.boundary_features(lab, bnd)
@@ -40,3 +157,234 @@ def test_graph_only(gpu):
     out = rag.rag_features(lab)
     np.testing.assert_array_equal(out['edges'], O.rag_edges(lab))
     np.testing.assert_array_equal(out['nodes'], O.unique_labels(lab))
+
+
+def test_label_bits_32(gpu):
+    lab, bnd = S.generate((20, 40, 50), cell=5, seed=8)
+    e_ref, f_ref = O.boundary_features(lab, bnd)
+    out = rag.rag_features(lab.astype(np.uint32), bnd)
+    np.testing.assert_array_equal(out['edges'], e_ref)
+    np.testing.assert_array_equal(out['nodes'], O.unique_labels(lab))
+    check_features(out['features'], f_ref)
+
+
+def test_values_outside_range_and_custom_range(gpu):
+    lab, bnd = S.generate((16, 30, 30), cell=5, seed=2)
+    data = (bnd * 3.0 - 1.0).astype(np.float32)     # [-1, 2]: both outlier slots populated
+    e_ref, f_ref = O.boundary_features(lab, data)
+    out = rag.rag_features(lab, data)
+    np.testing.assert_array_equal(out['edges'], e_ref)
+    check_features(out['features'], f_ref)
+    e_ref, f_ref = O.boundary_features(lab, data, lo=-1.0, hi=2.0)
+    out = rag.rag_features(lab, data, hist_range=(-1.0, 2.0))
+    np.testing.assert_array_equal(out['edges'], e_ref)
+    f = out['features']
+    np.testing.assert_array_equal(f[:, 9], f_ref[:, 9])
+    np.testing.assert_array_less(np.abs(f[:, 3:8] - f_ref[:, 3:8]), 3.0 / 40 + 1e-12)
+
+
+def test_single_label_and_empty(gpu):
+    lab = np.full((5, 6, 7), 42, np.uint64)
+    out = rag.rag_features(lab, np.zeros(lab.shape, np.float32))
+    assert out['edges'].shape == (0, 2) and out['features'].shape == (0, 10)
+    np.testing.assert_array_equal(out['nodes'], [42])
+    out = rag.rag_features(np.zeros((0, 4, 4), np.uint64))
+    assert out['edges'].shape == (0, 2) and out['nodes'].shape == (0,)
+
+
+def test_many_edges_per_tile(gpu):
+    """cell 2: dense supervoxels, the LDS edge table overflows into direct records."""
+    lab, bnd = S.generate((24, 64, 128), cell=2, seed=6)
+    e_ref, f_ref = O.boundary_features(lab, bnd)
+    out = rag.rag_features(lab, bnd)
+    np.testing.assert_array_equal(out['edges'], e_ref)
+    check_features(out['features'], f_ref)
+
+
+def test_salt_and_pepper_labels(gpu):
+    """Random labels: almost every face is a boundary face with a new key."""
+    rng = np.random.default_rng(1)
+    lab = rng.integers(0, 50, size=(12, 40, 70)).astype(np.uint64)
+    bnd = rng.random(lab.shape).astype(np.float32)
+    e_ref, f_ref = O.boundary_features(lab, bnd)
+    out = rag.rag_features(lab, bnd)
+    np.testing.assert_array_equal(out['edges'], e_ref)
+    check_features(out['features'], f_ref)
+    lab = rng.integers(0, 100000, size=(12, 40, 70)).astype(np.uint64)
+    e_ref, f_ref = O.boundary_features(lab, bnd)
+    out = rag.rag_features(lab, bnd)
+    np.testing.assert_array_equal(out['edges'], e_ref)
+    check_features(out['features'], f_ref)
+
+
+@pytest.mark.parametrize('offsets', [S.NN_OFFSETS, S.LR_OFFSETS])
+def test_affinity_random_volumes(gpu, offsets):
+    lab, bnd = S.generate((20, 60, 60), cell=6, seed=12)
+    affs = S.affinities_from_boundary(bnd, offsets)
+    e_ref, f_ref = O.affinity_features(lab, affs, offsets)
+    out = rag.rag_features(lab, affs, offsets=offsets)
+    np.testing.assert_array_equal(out['edges'], e_ref)
+    check_features(out['features'], f_ref)
+    # uint8 affinities
+    a8 = np.round(affs * 255).astype(np.uint8)
+    e_ref, f_ref = O.affinity_features(lab, a8, offsets)
+    out = rag.rag_features(lab, a8, offsets=offsets)
+    np.testing.assert_array_equal(out['edges'], e_ref)
+    check_features(out['features'], f_ref)
+
+
+def test_affinity_edge_list_filter(gpu):
+    """no_adj_filter + an explicit edge list = the ndist per-block semantics."""
+    lab, bnd = S.generate((16, 40, 40), cell=5, seed=13)
+    offs = S.LR_OFFSETS
+    affs = S.affinities_from_boundary(bnd, offs)
+    ob, oe = (1, 1, 1), (12, 30, 33)
+    edge_list = O.rag_edges(lab[:12, :30, :33])      # some block's sub-graph edges
+    e_ref, f_ref = O.affinity_features(lab, affs, offs, own_begin=ob, own_end=oe, edge_list=edge_list)
+    out = rag.rag_features(lab, affs, offsets=offs, own_begin=ob, own_end=oe, no_adj_filter=True)
+    rows = rag.map_edge_ids(out['edges'], e_ref)
+    hit = rows >= 0
+    f = np.zeros_like(f_ref)
+    f[hit] = out['features'][rows[hit]]
+    check_features(f, f_ref)
+
+
+# --------------------------------------------------------------- helpers
+def test_synth_matches_numpy(gpu):
+    import torch
+    shape, gshape = (9, 33, 47), (30, 33, 47)
+    lab_t, bnd_t = rag.synth_volume(shape, cell=6, seed=4, z_offset=11, global_shape=gshape)
+    lab, bnd = S.generate(shape, cell=6, seed=4, z_offset=11, global_shape=gshape)
+    np.testing.assert_array_equal(lab_t.cpu().numpy().view(np.uint64), lab)
+    np.testing.assert_array_equal(bnd_t.cpu().numpy(), bnd)
+    affs_t = rag.synth_affinities(bnd_t, S.LR_OFFSETS)
+    np.testing.assert_array_equal(affs_t.cpu().numpy(), S.affinities_from_boundary(bnd, S.LR_OFFSETS))
+    torch.cuda.synchronize()
+
+
+def test_device_tensors_in_and_out(gpu):
+    import torch
+    lab_t, bnd_t = rag.synth_volume((24, 50, 70), cell=6, seed=9)
+    r = rag.rag_features_handle(lab_t, bnd_t)
+    e_t, f_t = r.edges_torch_i64(), r.features_torch()
+    r.free()
+    lab, bnd = S.generate((24, 50, 70), cell=6, seed=9)
+    e_ref, f_ref = O.boundary_features(lab, bnd)
+    np.testing.assert_array_equal(e_t.cpu().numpy().view(np.uint64), e_ref)
+    check_features(f_t.cpu().numpy(), f_ref)
+    assert e_t.is_cuda and f_t.is_cuda and torch.cuda.current_device() == e_t.device.index
+
+
+def test_merge_stats_of_slabs_equals_whole(gpu):
+    lab, bnd = S.generate((30, 40, 44), cell=5, seed=14)
+    e_ref, f_ref = O.boundary_features(lab, bnd)
+    a = rag.rag_features(lab[:13], bnd[:13], keep_stats=True)
+    b = rag.rag_features(lab[12:], bnd[12:], own_begin=(1, 0, 0), keep_stats=True)
+    keys = np.concatenate([a['edges'], b['edges']])
+    sums = np.concatenate([a['sums'], b['sums']])
+    recs = np.concatenate([a['records'], b['records']])
+    m = rag.merge_stats(keys, sums, recs)
+    np.testing.assert_array_equal(m['edges'], e_ref)
+    check_features(m['features'], f_ref)
+
+
+def test_unique_and_map_helpers(gpu):
+    rng = np.random.default_rng(3)
+    v = rng.integers(0, 2 ** 40, size=5000).astype(np.uint64)
+    r = rag.unique_values_handle(v)
+    np.testing.assert_array_equal(r.nodes(), np.unique(v))
+    r.free()
+    pairs = np.sort(rng.integers(0, 300, size=(4000, 2)), axis=1).astype(np.uint64)
+    pairs = pairs[pairs[:, 0] != pairs[:, 1]]
+    e, n = rag.unique_pairs(pairs)
+    np.testing.assert_array_equal(e, O._unique_pairs(pairs))
+    np.testing.assert_array_equal(n, np.unique(pairs))
+    q = np.concatenate([e[::7], np.array([[1000, 1001], [0, 0]], np.uint64)])
+    ids = rag.map_edge_ids(e, q)
+    np.testing.assert_array_equal(ids, O.find_edges(e, q))
+    assert ids[-1] == -1 and ids[-2] == -1
+    lab = rng.integers(0, 60, size=(9, 10, 11)).astype(np.uint64)
+    np.testing.assert_array_equal(rag.unique_labels(lab, (2, 3, 4), (7, 9, 10)), np.unique(lab[2:7, 3:9, 4:10]))
+
+
+def test_hip_backend_slabs_merge(gpu):
+    """The multi-GPU data path (local partials -> packed rows -> merge) on one
+    GPU: two slabs processed by HipBackend, rows packed/unpacked as dist.py
+    ships them, merged on the device == whole volume."""
+    import torch
+    from cluster_tools_amd import dist as cdist
+    shape = (40, 48, 56)
+    lab, bnd = rag.synth_volume(shape, cell=6, seed=21)
+    be = cdist.HipBackend()
+    parts = []
+    for z0, z1 in ((0, 17), (17, 40)):
+        h = 1 if z0 else 0
+        k, s, r, n, _ = be.local(lab[z0 - h:z1].contiguous(), bnd[z0 - h:z1].contiguous(), None,
+                                 (h, 0, 0), None, False, (0.0, 1.0))
+        parts.append(cdist.pack_rows(k, s, r))
+    k, s, r = cdist.unpack_rows(torch.cat(parts))
+    m = be.merge(k, s, r, (0.0, 1.0))
+    e_ref, f_ref = O.boundary_features(lab.cpu().numpy().view(np.uint64), bnd.cpu().numpy())
+    np.testing.assert_array_equal(m.edges(), e_ref)
+    check_features(m.features(), f_ref)
+    m.free()
+
+
+def test_hip_backend_affinity_slabs_merge(gpu):
+    import torch
+    from cluster_tools_amd import dist as cdist
+    shape = (30, 40, 40)
+    lab, bnd = rag.synth_volume(shape, cell=5, seed=22)
+    offs = [[-1, 0, 0], [0, -1, 0], [0, 0, -1], [-2, 0, 0], [0, -3, 0], [0, 0, -3]]
+    affs = rag.synth_affinities(bnd, offs)
+    be = cdist.HipBackend()
+    parts = []
+    for z0, z1 in ((0, 13), (13, 30)):
+        h = 2 if z0 else 0                                # halo = max |z offset|
+        k, s, r, n, _ = be.local(lab[z0 - h:z1].contiguous(), affs[:, z0 - h:z1].contiguous(), offs,
+                                 (h, 0, 0), None, False, (0.0, 1.0))
+        parts.append(cdist.pack_rows(k, s, r))
+    k, s, r = cdist.unpack_rows(torch.cat(parts))
+    m = be.merge(k, s, r, (0.0, 1.0))
+    e_ref, f_ref = O.affinity_features(lab.cpu().numpy().view(np.uint64), affs.cpu().numpy(), offs)
+    np.testing.assert_array_equal(m.edges(), e_ref)
+    check_features(m.features(), f_ref)
+    m.free()
+
+
+# ------------------------------------------------------- labels >= 2^32
+BIG = np.uint64(1) << np.uint64(40)
+
+
+def test_labels_above_2_32(gpu):
+    """Labels >= 2^32 take the dense-relabelling path."""
+    lab, bnd = S.generate((18, 40, 44), cell=5, seed=15)
+    big = lab * np.uint64(977) + BIG          # sparse, huge ids; same partition
+    e_ref, f_ref = O.boundary_features(lab, bnd)
+    out = rag.rag_features(big, bnd)
+    np.testing.assert_array_equal(out['edges'], e_ref * np.uint64(977) + BIG)
+    np.testing.assert_array_equal(out['nodes'], O.unique_labels(lab) * np.uint64(977) + BIG)
+    check_features(out['features'], f_ref)
+    g = rag.rag_features(big)
+    np.testing.assert_array_equal(g['edges'], e_ref * np.uint64(977) + BIG)
+    offs = S.NN_OFFSETS
+    affs = S.affinities_from_boundary(bnd, offs)
+    e_ref, f_ref = O.affinity_features(lab, affs, offs)
+    out = rag.rag_features(big, affs, offsets=offs)
+    np.testing.assert_array_equal(out['edges'], e_ref * np.uint64(977) + BIG)
+    check_features(out['features'], f_ref)
+
+
+def test_merge_and_pairs_above_2_32(gpu):
+    lab, bnd = S.generate((20, 30, 30), cell=5, seed=16)
+    big = lab + BIG
+    e_ref, f_ref = O.boundary_features(lab, bnd)
+    a = rag.rag_features(big[:9], bnd[:9], keep_stats=True)
+    b = rag.rag_features(big[8:], bnd[8:], own_begin=(1, 0, 0), keep_stats=True)
+    m = rag.merge_stats(np.concatenate([a['edges'], b['edges']]), np.concatenate([a['sums'], b['sums']]),
+                        np.concatenate([a['records'], b['records']]))
+    np.testing.assert_array_equal(m['edges'], e_ref + BIG)
+    check_features(m['features'], f_ref)
+    e, n = rag.unique_pairs(np.concatenate([a['edges'], b['edges']]))
+    np.testing.assert_array_equal(e, e_ref + BIG)
+    np.testing.assert_array_equal(n, np.unique(e_ref) + BIG)
