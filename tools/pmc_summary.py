@@ -1,0 +1,82 @@
+"""Summarise rocprofv3 CSV output into profiles/<round>/*.json.
+
+usage: python tools/pmc_summary.py <trace_dir> <pmc_dir_fetch> <pmc_dir_write> <out.json> [algorithmic_bytes]
+
+* kernel stats: <trace_dir>/**/*kernel_stats.csv (Name, Calls, AverageNs ...)
+* PMC: <pmc_dir>/**/*counter_collection.csv, one row per (dispatch, counter)
+FETCH_SIZE / WRITE_SIZE are in KiB per dispatch.  gfx950 tallies 128-B read
+requests at 64 B (MI355X_MICROARCH.md, HBM section), so the HBM read bytes of
+a coalesced stream are 2 x FETCH_SIZE x 1024; the factor is re-derived from
+the loads-only ablation of the face scan when that pass is present.
+"""
+import csv
+import glob
+import json
+import os
+import sys
+
+
+def _rows(pattern):
+    out = []
+    for f in sorted(glob.glob(pattern, recursive=True)):
+        with open(f) as fh:
+            out.extend(csv.DictReader(fh))
+    return out
+
+
+def kernel_stats(d):
+    res = {}
+    for r in _rows(os.path.join(d, '**', '*kernel_stats.csv')):
+        name = r.get('Name') or r.get('KernelName') or ''
+        res[name] = {'calls': int(r['Calls']), 'avg_ns': float(r['AverageNs']),
+                     'total_ns': float(r['TotalDurationNs']), 'pct': float(r.get('Percentage', 0.0))}
+    return res
+
+
+def counter_per_dispatch(d, counter):
+    acc = {}
+    for r in _rows(os.path.join(d, '**', '*counter_collection.csv')):
+        if r.get('Counter_Name') != counter:
+            continue
+        name = r.get('Kernel_Name', '')
+        acc.setdefault(name, []).append(float(r['Counter_Value']))
+    return {k: sum(v) / len(v) for k, v in acc.items()}
+
+
+def pick(d, sub):
+    for k, v in d.items():
+        if sub in k:
+            return v
+    return None
+
+
+def main():
+    trace, pf, pw, out = sys.argv[1:5]
+    alg = float(sys.argv[5]) if len(sys.argv) > 5 else None
+    stats = kernel_stats(trace)
+    fetch = counter_per_dispatch(pf, 'FETCH_SIZE')
+    write = counter_per_dispatch(pw, 'WRITE_SIZE')
+    scan_f = pick(fetch, 'k_face_scan')
+    scan_w = pick(write, 'k_face_scan')
+    summary = {
+        'kernel_stats': stats,
+        'fetch_size_kib_per_dispatch': fetch,
+        'write_size_kib_per_dispatch': write,
+        'read_factor': 2.0,
+        'note': 'HBM bytes = 2 x FETCH_SIZE x 1024 + WRITE_SIZE x 1024 (gfx950 FETCH_SIZE halving)',
+    }
+    if scan_f is not None and scan_w is not None:
+        summary['scan_hbm_bytes_per_launch'] = 2.0 * scan_f * 1024 + scan_w * 1024
+        summary['scan_read_bytes_per_launch'] = 2.0 * scan_f * 1024
+        summary['scan_write_bytes_per_launch'] = scan_w * 1024
+        if alg:
+            summary['scan_algorithmic_bytes'] = alg
+            summary['scan_traffic_over_algorithmic'] = summary['scan_hbm_bytes_per_launch'] / alg
+    os.makedirs(os.path.dirname(out) or '.', exist_ok=True)
+    with open(out, 'w') as fh:
+        json.dump(summary, fh, indent=1, sort_keys=True)
+    print(json.dumps({k: v for k, v in summary.items() if k.startswith('scan')}))
+
+
+if __name__ == '__main__':
+    main()
