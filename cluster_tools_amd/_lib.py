@@ -11,7 +11,7 @@ import os
 import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, 'libctg.so')
+LIB_PATH = os.environ.get('CTG_LIB') or os.path.join(_HERE, 'libctg.so')  # CTG_LIB: A/B builds (tools/)
 
 CTG_OK = 0
 CTG_MEM_HOST = 0

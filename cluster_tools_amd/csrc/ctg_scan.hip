@@ -255,8 +255,13 @@ __device__ __forceinline__ bool make_key(bool act, LabelT a, LabelT b, uint64_t&
 // 64 entries, the wave takes the staged faces one per lane and folds them into
 // the edge table (home-bucket probe, statistics atomics, histogram).  Every
 // lane of a batch carries a face, instead of ~1 in 10 lanes of a site.
+#ifdef CTG_FOLD_NOINLINE
+#define CTG_FOLD_INLINE __noinline__
+#else
+#define CTG_FOLD_INLINE __forceinline__
+#endif
 template <int MODE>
-__device__ __forceinline__ void fold_batch(Table& T, const uint4* __restrict__ stage, int nb, int lane, RecordBuf R,
+__device__ CTG_FOLD_INLINE void fold_batch(Table& T, const uint4* __restrict__ stage, int nb, int lane, RecordBuf R,
                                            Counters* C, bool fast40, double scale, double offset, int ablate) {
     constexpr bool BND = MODE == MODE_BOUNDARY;
     constexpr bool AFF = MODE == MODE_AFFINITY;

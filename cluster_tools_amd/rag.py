@@ -49,7 +49,7 @@ class Result:
         self.free()
 
     def free(self):
-        if getattr(self, 'handle', None):
+        if getattr(self, 'handle', None) and L is not None:
             L.load().ctg_free(self.handle)
             self.handle = None
 

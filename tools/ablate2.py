@@ -1,0 +1,30 @@
+"""Timing of the face scan under CTG_ABLATE values given on the command line
+(each in a child process; stderr carries the s_memtime stamp line for 256)."""
+import json, os, subprocess, sys
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if len(sys.argv) > 1 and sys.argv[1] == '--child':
+    sys.path.insert(0, ROOT)
+    import torch
+    from cluster_tools_amd import rag
+    S = int(os.environ.get('CTG_PROF_SIZE', '512'))
+    lab, bnd = rag.synth_volume((S, S, S), cell=int(os.environ.get('CTG_PROF_CELL', '10')))
+    torch.cuda.synchronize()
+    r = None
+    for i in range(3):
+        if r: r.free()
+        r = rag.rag_features_handle(lab, bnd)
+    rag.set_profiling(True)
+    ts = []
+    for i in range(5):
+        r.free(); r = rag.rag_features_handle(lab, bnd); ts.append(rag.last_timings())
+    print(json.dumps({'lib': os.path.basename(os.environ.get('CTG_LIB', 'libctg.so')),
+                      'ablate': os.environ.get('CTG_ABLATE', '0'), 'records': r.info()[0],
+                      **{k: round(sum(t[k] for t in ts) / len(ts), 4) for k in ts[0]}}), flush=True)
+else:
+    # spec: "<ablate>" or "<variant>@<ablate>" (variant -> variants/libctg_<variant>.so)
+    for spec in sys.argv[1:]:
+        var, _, ab = spec.rpartition('@')
+        env = dict(os.environ, CTG_ABLATE=ab or '0')
+        if var:
+            env['CTG_LIB'] = os.path.join(ROOT, 'variants', 'libctg_%s.so' % var)
+        subprocess.run([sys.executable, os.path.abspath(__file__), '--child'], env=env, check=True)
