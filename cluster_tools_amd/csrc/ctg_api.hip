@@ -16,6 +16,7 @@
 
 namespace ctg {
 hipError_t launch_face_scan(const ScanParams& P, const RecordBuf& R, Counters* C, hipStream_t s);
+int scan_tile_rows();
 hipError_t launch_unique_tiles(const uint64_t* L, const int64_t* shape, const int64_t* b, const int64_t* e,
                                uint64_t* out, unsigned long long* count, int64_t cap, hipStream_t s);
 hipError_t launch_pack_keys(int64_t n, const uint64_t* key, int nb, uint64_t* sk, uint32_t* idx, hipStream_t s);
@@ -529,18 +530,14 @@ int ctg_rag_features(const void* labels, int label_bits, const void* data, int d
     P.scale = (double)NBINS / (hist_hi - hist_lo);
     P.offset = hist_lo;
     P.fast40 = (hist_lo == 0.0 && P.scale == 40.0) ? 1 : 0;
-    // A u16 histogram slot gains at most spv samples per voxel of one plane of
-    // the 64x32 tile cross-section; the scan flushes its LDS table before any
-    // entry could reach 65535 within the next plane.
-    const int spv = P.n_channels > 0 ? std::max(P.n_channels, 3) : 6;
-    // (plus 2 samples for each of the 64 staged faces of each of the 8 waves)
-    // (checked every 4 planes, plus 2 samples for each of the 64 staged faces
-    // of each of the 8 waves)
-    P.check_planes = std::max(1, std::min(4, (65535 - 2 * 64 * 8) / (spv * TILE_X * 32)));
-    P.hist_guard = (uint32_t)(65535 - P.check_planes * spv * TILE_X * 32 - 2 * 64 * 8);
+    // flush decisions every check_planes planes (overflow safety does not
+    // depend on it: ctg_scan.hip bounds each entry's count in the fold)
+    P.check_planes = 2;
+    if (const char* cp = getenv("CTG_CHECK_PLANES")) P.check_planes = std::max(1, atoi(cp));
     // planes per workgroup: deep tiles (fewer records), but >= ~1024 workgroups
     {
-        const int64_t cols = ((shape[2] + TILE_X - 1) / TILE_X) * ((shape[1] + 31) / 32);
+        const int64_t rows = scan_tile_rows();
+        const int64_t cols = ((shape[2] + TILE_X - 1) / TILE_X) * ((shape[1] + rows - 1) / rows);
         int tz = 64;
         while (tz > 8 && cols * ((shape[0] + tz - 1) / tz) < 1024) tz /= 2;
         P.tile_z = tz;
@@ -588,9 +585,6 @@ int ctg_rag_features(const void* labels, int label_bits, const void* data, int d
     const int64_t n = (int64_t)w.counters_host->n_records;
     w.last_records = n;
     w.last_direct = (int64_t)w.counters_host->n_direct;
-    if (P.ablate & 256)
-        fprintf(stderr, "ctg stamps (wave-cycles): total %llu fold %llu flush %llu check-barrier %llu\n",
-                w.counters_host->pad[0], w.counters_host->pad[2], w.counters_host->pad[3], w.counters_host->pad[1]);
 
     ctg_result* r = new ctg_result();
     r->device = dev;

@@ -82,10 +82,9 @@ struct ScanParams {
     double scale, offset;      // histogram mapping
     double u8_scale;           // uint8 -> float factor (1/255)
     int tile_z;                // z-planes per workgroup
-    uint32_t hist_guard;       // flush before a u16 histogram slot can wrap
     int check_planes;          // planes between flush decisions
     int fast40;                // histogram range [0,1) x 40 bins: exact f32 binning
-    int ablate;                // diagnostic: 8 loads only, 16 no per-plane barrier
+    int ablate;                // diagnostic: 8 loads only, 32 staging without fold
 };
 
 struct Counters {               // device-side counters, zeroed per call
