@@ -22,17 +22,19 @@ hipError_t launch_unique_tiles(const uint64_t* L, const int64_t* shape, const in
 hipError_t launch_pack_keys(int64_t n, const uint64_t* key, int nb, uint64_t* sk, uint32_t* idx, hipStream_t s);
 hipError_t launch_pack_pairs(int64_t n, const uint64_t* uv, int nb, uint64_t* sk, uint32_t* idx, hipStream_t s);
 hipError_t launch_max_pairs(int64_t n, const uint64_t* uv, unsigned long long* out, hipStream_t s);
-hipError_t launch_reduce(int64_t E, const uint64_t* uniq, const uint32_t* runs, const uint32_t* offs,
-                         const uint32_t* perm, const RecordBuf& R, int wide, int stats, int nb, int need_adj,
-                         int ignore_label, double scale, double offset, const ReduceOut& O, hipStream_t s);
-hipError_t launch_compact(int64_t E, const uint32_t* keep, const uint32_t* pos, const ReduceOut& in,
-                          const ReduceOut& out, hipStream_t s);
+hipError_t launch_reduce(int64_t E, const uint32_t* dE, const uint64_t* uniq, const uint32_t* runs,
+                         const uint32_t* offs, const uint32_t* perm, const RecordBuf& R, int wide, int stats, int nb,
+                         int need_adj, int ignore_label, double scale, double offset, const ReduceOut& O,
+                         hipStream_t s);
+hipError_t launch_compact(int64_t E, const uint32_t* dE, const uint32_t* keep, const uint32_t* pos,
+                          const ReduceOut& in, const ReduceOut& out, uint32_t* dkept, hipStream_t s);
 hipError_t launch_endpoints(int64_t E, const uint64_t* uniq, int nb, uint32_t* out, hipStream_t s);
 hipError_t launch_u32_to_u64(int64_t n, const uint32_t* in, uint64_t* out, hipStream_t s);
-hipError_t launch_mark_nodes(int64_t E, const uint64_t* uniq, int nb, uint32_t* bits, hipStream_t s);
+hipError_t launch_mark_nodes(int64_t E, const uint32_t* dE, const uint64_t* uniq, int nb, uint32_t* bits,
+                             hipStream_t s);
 hipError_t launch_popc_words(int64_t W, const uint32_t* bits, uint32_t* cnt, hipStream_t s);
 hipError_t launch_bits_to_nodes(int64_t W, const uint32_t* bits, const uint32_t* off, uint64_t* nodes,
-                                hipStream_t s);
+                                const uint32_t* cnt, uint32_t* dN, hipStream_t s);
 hipError_t launch_find_edges(const uint64_t* ge, int64_t n, const uint64_t* q, int64_t m, int64_t* out,
                              hipStream_t s);
 hipError_t launch_synth(uint64_t* labels, float* boundary, const int64_t* shape, int64_t z_offset,
@@ -144,11 +146,11 @@ hipError_t ensure_records(Workspace& w, int64_t need, int wide) {
     dfree(w.rec.key);
     dfree(w.rec.sums);
     dfree(w.rec.hist);
-    const int words = wide ? WREC_WORDS : NREC_WORDS;
+    const int words = wide ? WREC_WORDS : NREC_STRIDE;
     w.rec.key = (uint64_t*)dalloc((size_t)need * 8);
-    w.rec.sums = (double2*)dalloc((size_t)need * 16);
+    w.rec.sums = wide ? (double2*)dalloc((size_t)need * 16) : nullptr;
     w.rec.hist = (uint32_t*)dalloc((size_t)need * words * 4);
-    if (!w.rec.key || !w.rec.sums || !w.rec.hist) return hipErrorOutOfMemory;
+    if (!w.rec.key || (wide && !w.rec.sums) || !w.rec.hist) return hipErrorOutOfMemory;
     w.rec.cap = need;
     return hipSuccess;
 }
@@ -199,13 +201,37 @@ struct ReduceJob {
 };
 
 static hipError_t reduce_records(Workspace& w, const ReduceJob& J, hipStream_t s, ctg_result* res) {
+    // Device-resident counts: the run count E_all, the kept edge count E and
+    // the node count N stay in w.small[0..2] until one read-back at the end;
+    // every kernel in between bounds itself by them, and buffers are sized by
+    // the record count n (an upper bound), so the back half issues no
+    // host synchronisation (except on the rare node path for labels >= 2^30).
     Ev ev{w, s};
     const int64_t n = J.n;
     const int nb = bits_for(J.max_v);
     if (nb > 32) return hipErrorInvalidValue;
+    if (n == 0) {
+        res->n_edges = 0;
+        res->edges = (uint64_t*)dalloc(16);
+        res->features = J.stats ? (double*)dalloc(N_FEATURES * 8) : nullptr;
+        if (J.keep_stats && J.stats) {
+            res->stats = (uint32_t*)dalloc(WREC_WORDS * 4);
+            res->stat_sums = (double2*)dalloc(16);
+        }
+        res->nodes = (uint64_t*)dalloc(8);
+        res->n_nodes = 0;
+        if (J.single_label_ptr) {
+            hipError_t e = hipMemcpyAsync(res->nodes, J.single_label_ptr, 8, hipMemcpyDeviceToDevice, s);
+            if (e != hipSuccess) return e;
+            res->n_nodes = 1;
+        }
+        for (int i = 2; i <= 6; ++i) ev.mark(i);
+        return hipStreamSynchronize(s);
+    }
     // sort buffers
     if (n > w.sort_cap) {
         dfree(w.sk_in); dfree(w.sk_out); dfree(w.idx_in); dfree(w.idx_out);
+        dfree(w.uniq); dfree(w.runs); dfree(w.offs); dfree(w.keep); dfree(w.pos);
         const int64_t cap = std::max<int64_t>(n, w.sort_cap + w.sort_cap / 2);
         w.sk_in = (uint64_t*)dalloc(cap * 8); w.sk_out = (uint64_t*)dalloc(cap * 8);
         w.idx_in = (uint32_t*)dalloc(cap * 4); w.idx_out = (uint32_t*)dalloc(cap * 4);
@@ -216,6 +242,9 @@ static hipError_t reduce_records(Workspace& w, const ReduceJob& J, hipStream_t s
             return hipErrorOutOfMemory;
         w.sort_cap = cap;
     }
+    uint32_t* dE_all = w.small;
+    uint32_t* dE = w.small + 1;
+    uint32_t* dN = w.small + 2;
     hipError_t e;
     if (J.keys) e = launch_pack_keys(n, J.keys, nb, w.sk_in, w.idx_in, s);
     else e = launch_pack_pairs(n, J.pairs, nb, w.sk_in, w.idx_in, s);
@@ -224,119 +253,113 @@ static hipError_t reduce_records(Workspace& w, const ReduceJob& J, hipStream_t s
     ROCPRIM_CALL(w, rocprim::radix_sort_pairs(t, tbytes, w.sk_in, w.sk_out, w.idx_in, w.idx_out, (size_t)n, 0u,
                                               (unsigned)(2 * nb), s));
     ev.mark(3);
-    ROCPRIM_CALL(w, rocprim::run_length_encode(t, tbytes, w.sk_out, (unsigned)n, w.uniq, w.runs, w.small, s));
-    e = hipMemcpyAsync(w.small_host, w.small, sizeof(unsigned), hipMemcpyDeviceToHost, s);
-    if (e != hipSuccess) return e;
-    e = hipStreamSynchronize(s);
-    if (e != hipSuccess) return e;
-    const int64_t E_all = n ? (int64_t)w.small_host[0] : 0;
-    ROCPRIM_CALL(w, rocprim::exclusive_scan(t, tbytes, w.runs, w.offs, 0u, (size_t)E_all, rocprim::plus<uint32_t>(), s));
+    ROCPRIM_CALL(w, rocprim::run_length_encode(t, tbytes, w.sk_out, (unsigned)n, w.uniq, w.runs, dE_all, s));
+    // offsets over the n-bound: entries past E_all are never read
+    ROCPRIM_CALL(w, rocprim::exclusive_scan(t, tbytes, w.runs, w.offs, 0u, (size_t)n, rocprim::plus<uint32_t>(), s));
     ev.mark(4);
 
-    // outputs (uncompacted)
+    // outputs (uncompacted), sized by the bound n
     const bool may_drop = J.need_adj || J.ignore_label;
     ReduceOut O{};
-    O.edges = (uint64_t*)dalloc(std::max<int64_t>(E_all, 1) * 16);
-    O.feats = J.stats ? (double*)dalloc(std::max<int64_t>(E_all, 1) * N_FEATURES * 8) : nullptr;
+    O.edges = (uint64_t*)dalloc(n * 16);
+    O.feats = J.stats ? (double*)dalloc(n * N_FEATURES * 8) : nullptr;
     O.keep = may_drop ? w.keep : nullptr;
     if (J.keep_stats && J.stats) {
-        O.wstats = (uint32_t*)dalloc(std::max<int64_t>(E_all, 1) * WREC_WORDS * 4);
-        O.wsums = (double2*)dalloc(std::max<int64_t>(E_all, 1) * 16);
+        O.wstats = (uint32_t*)dalloc(n * WREC_WORDS * 4);
+        O.wsums = (double2*)dalloc(n * 16);
     }
-    e = launch_reduce(E_all, w.uniq, w.runs, w.offs, w.idx_out, J.R, J.wide, J.stats, nb, J.need_adj,
+    if (!O.edges || (J.stats && !O.feats)) return hipErrorOutOfMemory;
+    e = launch_reduce(n, dE_all, w.uniq, w.runs, w.offs, w.idx_out, J.R, J.wide, J.stats, nb, J.need_adj,
                       J.ignore_label, J.scale, J.offset, O, s);
     if (e != hipSuccess) return e;
-    int64_t E = E_all;
-    if (may_drop && E_all) {
-        ROCPRIM_CALL(w, rocprim::exclusive_scan(t, tbytes, w.keep, w.pos, 0u, (size_t)E_all, rocprim::plus<uint32_t>(), s));
-        unsigned tail[2];
-        e = hipMemcpyAsync(w.small_host, w.pos + (E_all - 1), 4, hipMemcpyDeviceToHost, s);
-        if (e != hipSuccess) return e;
-        e = hipMemcpyAsync(w.small_host + 1, w.keep + (E_all - 1), 4, hipMemcpyDeviceToHost, s);
-        if (e != hipSuccess) return e;
-        e = hipStreamSynchronize(s);
-        if (e != hipSuccess) return e;
-        tail[0] = w.small_host[0];
-        tail[1] = w.small_host[1];
-        E = (int64_t)tail[0] + tail[1];
-        if (E != E_all) {
-            ReduceOut C2{};
-            C2.edges = (uint64_t*)dalloc(std::max<int64_t>(E, 1) * 16);
-            C2.feats = O.feats ? (double*)dalloc(std::max<int64_t>(E, 1) * N_FEATURES * 8) : nullptr;
-            if (O.wstats) {
-                C2.wstats = (uint32_t*)dalloc(std::max<int64_t>(E, 1) * WREC_WORDS * 4);
-                C2.wsums = (double2*)dalloc(std::max<int64_t>(E, 1) * 16);
-            }
-            e = launch_compact(E_all, w.keep, w.pos, O, C2, s);
-            if (e != hipSuccess) return e;
-            e = hipStreamSynchronize(s);
-            if (e != hipSuccess) return e;
-            dfree(O.edges); dfree(O.feats); dfree(O.wstats); dfree(O.wsums);
-            O = C2;
+    if (may_drop) {
+        ROCPRIM_CALL(w, rocprim::exclusive_scan(t, tbytes, w.keep, w.pos, 0u, (size_t)n, rocprim::plus<uint32_t>(), s));
+        ReduceOut C2{};
+        C2.edges = (uint64_t*)dalloc(n * 16);
+        C2.feats = O.feats ? (double*)dalloc(n * N_FEATURES * 8) : nullptr;
+        if (O.wstats) {
+            C2.wstats = (uint32_t*)dalloc(n * WREC_WORDS * 4);
+            C2.wsums = (double2*)dalloc(n * 16);
         }
+        e = launch_compact(n, dE_all, w.keep, w.pos, O, C2, dE, s);
+        if (e != hipSuccess) return e;
+        dfree(O.edges); dfree(O.feats); dfree(O.wstats); dfree(O.wsums);   // stream-ordered reuse
+        O = C2;
+    } else {
+        e = hipMemcpyAsync(dE, dE_all, 4, hipMemcpyDeviceToDevice, s);
+        if (e != hipSuccess) return e;
     }
     ev.mark(5);
-    res->n_edges = E;
     res->edges = O.edges;
     res->features = O.feats;
     res->stats = O.wstats;
     res->stat_sums = O.wsums;
 
     // nodes = unique endpoints of every unique key (before filtering)
-    if (E_all > 0 && J.max_v < (1ull << 30)) {
+    uint32_t counts[3] = {0, 0, 0};
+    if (J.max_v < (1ull << 30)) {
         // bitmap over [0, max label]: one pass over the sorted key table
         const int64_t W = (int64_t)(J.max_v >> 5) + 1;
         uint32_t* bits = (uint32_t*)dalloc(W * 4);
         uint32_t* cnt = (uint32_t*)dalloc(W * 4);
         uint32_t* off = (uint32_t*)dalloc(W * 4);
-        if (!bits || !cnt || !off) return hipErrorOutOfMemory;
+        res->nodes = (uint64_t*)dalloc(std::min<int64_t>(W * 32, 2 * n) * 8);
+        if (!bits || !cnt || !off || !res->nodes) return hipErrorOutOfMemory;
         e = hipMemsetAsync(bits, 0, W * 4, s);
         if (e != hipSuccess) return e;
-        e = launch_mark_nodes(E_all, w.uniq, nb, bits, s);
+        e = launch_mark_nodes(n, dE_all, w.uniq, nb, bits, s);
         if (e != hipSuccess) return e;
         e = launch_popc_words(W, bits, cnt, s);
         if (e != hipSuccess) return e;
         ROCPRIM_CALL(w, rocprim::exclusive_scan(t, tbytes, cnt, off, 0u, (size_t)W, rocprim::plus<uint32_t>(), s));
-        e = hipMemcpyAsync(w.small_host + 1, off + (W - 1), 4, hipMemcpyDeviceToHost, s);
+        e = launch_bits_to_nodes(W, bits, off, res->nodes, cnt, dN, s);
         if (e != hipSuccess) return e;
-        e = hipMemcpyAsync(w.small_host + 2, cnt + (W - 1), 4, hipMemcpyDeviceToHost, s);
+        e = hipMemcpyAsync(w.small_host, w.small, 3 * sizeof(uint32_t), hipMemcpyDeviceToHost, s);
         if (e != hipSuccess) return e;
         e = hipStreamSynchronize(s);
         if (e != hipSuccess) return e;
-        const int64_t N = (int64_t)w.small_host[1] + w.small_host[2];
-        res->nodes = (uint64_t*)dalloc(std::max<int64_t>(N, 1) * 8);
-        e = launch_bits_to_nodes(W, bits, off, res->nodes, s);
-        if (e != hipSuccess) return e;
-        res->n_nodes = N;
+        for (int i = 0; i < 3; ++i) counts[i] = w.small_host[i];
         dfree(bits); dfree(cnt); dfree(off);
-    } else if (E_all > 0) {
-        uint32_t* ep = (uint32_t*)dalloc(E_all * 8);
-        uint32_t* ep2 = (uint32_t*)dalloc(E_all * 8);
-        uint32_t* nodes32 = (uint32_t*)dalloc(E_all * 8);
+    } else {
+        e = hipMemcpyAsync(w.small_host, w.small, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, s);
+        if (e != hipSuccess) return e;
+        e = hipStreamSynchronize(s);
+        if (e != hipSuccess) return e;
+        counts[0] = w.small_host[0];
+        counts[1] = w.small_host[1];
+        const int64_t E_all = counts[0];
+        uint32_t* ep = (uint32_t*)dalloc(std::max<int64_t>(E_all, 1) * 8);
+        uint32_t* ep2 = (uint32_t*)dalloc(std::max<int64_t>(E_all, 1) * 8);
+        uint32_t* nodes32 = (uint32_t*)dalloc(std::max<int64_t>(E_all, 1) * 8);
         if (!ep || !ep2 || !nodes32) return hipErrorOutOfMemory;
         e = launch_endpoints(E_all, w.uniq, nb, ep, s);
         if (e != hipSuccess) return e;
         ROCPRIM_CALL(w, rocprim::radix_sort_keys(t, tbytes, ep, ep2, (size_t)(2 * E_all), 0u, (unsigned)nb, s));
-        ROCPRIM_CALL(w, rocprim::unique(t, tbytes, ep2, nodes32, w.small + 1, (size_t)(2 * E_all),
+        ROCPRIM_CALL(w, rocprim::unique(t, tbytes, ep2, nodes32, dN, (size_t)(2 * E_all),
                                         rocprim::equal_to<uint32_t>(), s));
-        e = hipMemcpyAsync(w.small_host + 1, w.small + 1, 4, hipMemcpyDeviceToHost, s);
+        e = hipMemcpyAsync(w.small_host + 2, dN, 4, hipMemcpyDeviceToHost, s);
         if (e != hipSuccess) return e;
         e = hipStreamSynchronize(s);
         if (e != hipSuccess) return e;
-        const int64_t N = w.small_host[1];
-        res->nodes = (uint64_t*)dalloc(std::max<int64_t>(N, 1) * 8);
-        e = launch_u32_to_u64(N, nodes32, res->nodes, s);
+        counts[2] = w.small_host[2];
+        res->nodes = (uint64_t*)dalloc(std::max<int64_t>(counts[2], 1) * 8);
+        e = launch_u32_to_u64(counts[2], nodes32, res->nodes, s);
         if (e != hipSuccess) return e;
-        res->n_nodes = N;
+        e = hipStreamSynchronize(s);
+        if (e != hipSuccess) return e;
         dfree(ep); dfree(ep2); dfree(nodes32);
-    } else if (J.single_label_ptr) {
-        res->nodes = (uint64_t*)dalloc(8);
-        e = hipMemcpyAsync(res->nodes, J.single_label_ptr, 8, hipMemcpyDeviceToDevice, s);
-        if (e != hipSuccess) return e;
-        res->n_nodes = 1;
-    } else {
-        res->nodes = (uint64_t*)dalloc(8);
+    }
+    res->n_edges = counts[1];
+    res->n_nodes = counts[2];
+    if (counts[0] == 0) {   // no edge at all: the owned origin voxel's label is the only node
         res->n_nodes = 0;
+        if (J.single_label_ptr) {
+            e = hipMemcpyAsync(res->nodes, J.single_label_ptr, 8, hipMemcpyDeviceToDevice, s);
+            if (e != hipSuccess) return e;
+            e = hipStreamSynchronize(s);
+            if (e != hipSuccess) return e;
+            res->n_nodes = 1;
+        }
     }
     ev.mark(6);
     return hipSuccess;
@@ -532,7 +555,7 @@ int ctg_rag_features(const void* labels, int label_bits, const void* data, int d
     P.fast40 = (hist_lo == 0.0 && P.scale == 40.0) ? 1 : 0;
     // flush decisions every check_planes planes (overflow safety does not
     // depend on it: ctg_scan.hip bounds each entry's count in the fold)
-    P.check_planes = 2;
+    P.check_planes = 8;
     if (const char* cp = getenv("CTG_CHECK_PLANES")) P.check_planes = std::max(1, atoi(cp));
     // planes per workgroup: deep tiles (fewer records), but >= ~1024 workgroups
     {
@@ -610,7 +633,7 @@ int ctg_rag_features(const void* labels, int label_bits, const void* data, int d
                              ? (const uint64_t*)dl + ((o0 * shape[1] + o1) * shape[2] + o2)
                              : nullptr;
     hipError_t e = reduce_records(w, J, s, r);
-    if (e == hipSuccess && label_bits == 32 && r->n_edges == 0 && has_owned) {
+    if (e == hipSuccess && label_bits == 32 && r->n_records == 0 && has_owned) {
         // 32-bit labels: widen the single label
         uint32_t l32 = 0;
         e = hipMemcpyAsync(&l32, (const uint32_t*)dl + ((o0 * shape[1] + o1) * shape[2] + o2), 4,

@@ -23,6 +23,11 @@ constexpr int NBINS = 40;              // vigra UserRangeHistogram<40> (nifty de
 constexpr int NSLOTS = NBINS + 2;      // left outliers, 40 bins, right outliers
 constexpr int HWORDS = 21;             // 42 u16 slots packed in 21 u32 words
 constexpr int NREC_WORDS = 24;         // narrow record: 21 hist words + cnt + min + max
+// narrow records live in 128-byte bodies (one cache line each, so the
+// reduction's gather touches exactly one line per record):
+//   words 0..3 (sum f64, sum of squares f64), 4..27 the NREC_WORDS, 28..31 zero
+constexpr int NREC_STRIDE = 32;
+constexpr int NREC_OFF = 4;
 constexpr int WREC_WORDS = 48;         // wide record: 42 u32 slots + cnt + min + max + pad
 constexpr uint32_t ADJ_FLAG = 0x80000000u;  // record/edge came from a nearest-neighbour face
 constexpr uint64_t EMPTY_KEY = ~0ull;
@@ -64,8 +69,8 @@ __host__ __device__ inline uint32_t hash_key(uint64_t k) {
 // ---------------------------------------------------------------------------
 struct RecordBuf {
     uint64_t* key = nullptr;      // (u << 32) | v
-    double2* sums = nullptr;      // (sum, sum of squares)
-    uint32_t* hist = nullptr;     // NREC_WORDS (narrow) or WREC_WORDS (wide) per record
+    double2* sums = nullptr;      // wide records: (sum, sum of squares); narrow: unused (in the body)
+    uint32_t* hist = nullptr;     // narrow: NREC_STRIDE-word bodies; wide: WREC_WORDS per record
     int64_t cap = 0;
 };
 

@@ -10,6 +10,7 @@
 // (features/block_edge_features.py:146-147, features/merge_edge_features.py:62-65,
 // costs/probs_to_costs.py:205-207).
 #include <algorithm>
+#include <cstdlib>
 
 #include "ctg_internal.h"
 
@@ -112,13 +113,17 @@ __device__ void vigra_quantiles(const uint32_t* __restrict__ hl, double count, d
 
 template <bool WIDE>
 __device__ __forceinline__ void load_record(const RecordBuf& R, uint32_t i, uint32_t (&h)[NSLOTS], uint32_t& cnt,
-                                            uint32_t& flags, uint32_t& mn, uint32_t& mx) {
+                                            uint32_t& flags, uint32_t& mn, uint32_t& mx, double& sum, double& sq) {
     if constexpr (!WIDE) {
-        const uint4* p = (const uint4*)(R.hist + (size_t)i * NREC_WORDS);
+        // one 128-byte body: (sum, sumsq), then the 24 record words
+        const uint4* p = (const uint4*)(R.hist + (size_t)i * NREC_STRIDE);
+        const double2 sw = *reinterpret_cast<const double2*>(p);
+        sum += sw.x;
+        sq += sw.y;
         uint32_t w[NREC_WORDS];
 #pragma unroll
         for (int j = 0; j < NREC_WORDS / 4; ++j) {
-            uint4 v = p[j];
+            uint4 v = p[1 + j];
             w[4 * j] = v.x; w[4 * j + 1] = v.y; w[4 * j + 2] = v.z; w[4 * j + 3] = v.w;
         }
 #pragma unroll
@@ -144,18 +149,22 @@ __device__ __forceinline__ void load_record(const RecordBuf& R, uint32_t i, uint
         flags |= w[42] & ADJ_FLAG;
         mn = min(mn, w[43]);
         mx = max(mx, w[44]);
+        const double2 s2 = R.sums[i];
+        sum += s2.x;
+        sq += s2.y;
     }
 }
 
 template <bool WIDE, bool STATS>
-__global__ __launch_bounds__(256) void k_reduce_edges(int64_t E, const uint64_t* __restrict__ uniq,
+__global__ __launch_bounds__(256) void k_reduce_edges(int64_t E, const uint32_t* __restrict__ dE,
+                                                      const uint64_t* __restrict__ uniq,
                                                       const uint32_t* __restrict__ runs,
                                                       const uint32_t* __restrict__ offs,
                                                       const uint32_t* __restrict__ perm, RecordBuf R, int nb,
                                                       int need_adj, int ignore_label, double scale, double offset,
                                                       ReduceOut O) {
     const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (e >= E) return;
+    if (e >= E || e >= (int64_t)*dE) return;
     const uint64_t sk = uniq[e];
     const uint64_t u = sk >> nb, v = sk & ((1ull << nb) - 1ull);
     O.edges[2 * e] = u;
@@ -166,7 +175,7 @@ __global__ __launch_bounds__(256) void k_reduce_edges(int64_t E, const uint64_t*
             const uint32_t b = offs[e], n = runs[e];
             for (uint32_t r = b; r < b + n; ++r) {
                 const uint32_t i = perm[r];
-                flags |= R.hist[(size_t)i * (WIDE ? WREC_WORDS : NREC_WORDS) + (WIDE ? 42 : 21)] & ADJ_FLAG;
+                flags |= R.hist[(size_t)i * (WIDE ? WREC_WORDS : NREC_STRIDE) + (WIDE ? 42 : NREC_OFF + 21)] & ADJ_FLAG;
             }
         } else {
             flags = ADJ_FLAG;
@@ -182,10 +191,7 @@ __global__ __launch_bounds__(256) void k_reduce_edges(int64_t E, const uint64_t*
         const uint32_t b = offs[e], n = runs[e];
         for (uint32_t r = b; r < b + n; ++r) {
             const uint32_t i = perm[r];
-            load_record<WIDE>(R, i, h, cnt, flags, mn, mx);
-            const double2 s = R.sums[i];
-            sum += s.x;
-            sq += s.y;
+            load_record<WIDE>(R, i, h, cnt, flags, mn, mx, sum, sq);
         }
         // need_adj: 0 every record is an edge (boundary maps), 1 keep edges seen
         // on a nearest-neighbour face, 2 keep all and carry the flag (partials)
@@ -232,10 +238,13 @@ __global__ __launch_bounds__(256) void k_reduce_edges(int64_t E, const uint64_t*
     }
 }
 
-__global__ void k_compact(int64_t E, const uint32_t* __restrict__ keep, const uint32_t* __restrict__ pos,
-                          ReduceOut in, ReduceOut out) {
+__global__ void k_compact(int64_t E, const uint32_t* __restrict__ dE, const uint32_t* __restrict__ keep,
+                          const uint32_t* __restrict__ pos, ReduceOut in, ReduceOut out, uint32_t* __restrict__ kept) {
     const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (e >= E || !keep[e]) return;
+    const int64_t n = min(E, (int64_t)*dE);
+    if (e == n - 1) *kept = pos[e] + keep[e];   // kept edge count
+    if (n == 0 && e == 0) *kept = 0u;
+    if (e >= n || !keep[e]) return;
     const uint32_t p = pos[e];
     out.edges[2 * (size_t)p] = in.edges[2 * e];
     out.edges[2 * (size_t)p + 1] = in.edges[2 * e + 1];
@@ -260,9 +269,10 @@ __global__ void k_endpoints(int64_t E, const uint64_t* __restrict__ uniq, int nb
 
 // nodes as a bitmap over [0, max label]: u is sorted in the key table, so only
 // run heads mark it; every v marks its bit
-__global__ void k_mark_nodes(int64_t E, const uint64_t* __restrict__ uniq, int nb, uint32_t* __restrict__ bits) {
+__global__ void k_mark_nodes(int64_t E, const uint32_t* __restrict__ dE, const uint64_t* __restrict__ uniq, int nb,
+                             uint32_t* __restrict__ bits) {
     const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (e >= E) return;
+    if (e >= E || e >= (int64_t)*dE) return;
     const uint64_t sk = uniq[e];
     const uint32_t u = (uint32_t)(sk >> nb), v = (uint32_t)(sk & ((1ull << nb) - 1ull));
     if (e == 0 || (uint32_t)(uniq[e - 1] >> nb) != u) atomicOr(&bits[u >> 5], 1u << (u & 31));
@@ -275,8 +285,10 @@ __global__ void k_popc_words(int64_t W, const uint32_t* __restrict__ bits, uint3
 }
 
 __global__ void k_bits_to_nodes(int64_t W, const uint32_t* __restrict__ bits, const uint32_t* __restrict__ off,
-                                uint64_t* __restrict__ nodes) {
+                                uint64_t* __restrict__ nodes, const uint32_t* __restrict__ cnt,
+                                uint32_t* __restrict__ dN) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i == W - 1) *dN = off[i] + cnt[i];   // node count
     if (i >= W) return;
     uint32_t b = bits[i];
     uint32_t o = off[i];
@@ -287,9 +299,66 @@ __global__ void k_bits_to_nodes(int64_t W, const uint32_t* __restrict__ bits, co
     }
 }
 
-hipError_t launch_mark_nodes(int64_t E, const uint64_t* uniq, int nb, uint32_t* bits, hipStream_t s) {
+// Same bitmap, built per chunk of the sorted key table in LDS.  A chunk of
+// NODE_CHUNK consecutive edges covers a narrow u range and, for spatially
+// ordered label ids, a narrow v window above it: the workgroup marks its
+// nodes in an LDS window and ORs the non-zero words into the global bitmap
+// with coalesced atomics (one 256-B wave-instruction per 64 words), instead of
+// one scattered global atomic per edge.  A chunk whose v window does not fit
+// the LDS bitmap falls back to per-edge global atomics.
+constexpr int NODE_CHUNK = 2048;
+constexpr int NODE_WORDS = 8192;   // 32 KB LDS window = 262144 labels
+
+__global__ __launch_bounds__(256) void k_mark_nodes_win(int64_t E, const uint32_t* __restrict__ dE,
+                                                        const uint64_t* __restrict__ uniq, int nb,
+                                                        uint32_t* __restrict__ bits) {
+    __shared__ uint32_t bm[NODE_WORDS];
+    __shared__ uint32_t red[4];
+    const int tid = threadIdx.x;
+    E = min(E, (int64_t)*dE);
+    const int64_t e0 = (int64_t)blockIdx.x * NODE_CHUNK;
+    if (e0 >= E) return;
+    const int64_t e1 = min(E, e0 + NODE_CHUNK);
+    const uint64_t vmask = (1ull << nb) - 1ull;
+    const uint32_t base = (uint32_t)(uniq[e0] >> nb) & ~31u;   // v > u >= u(e0)
+    uint32_t vmax = 0;
+    for (int64_t e = e0 + tid; e < e1; e += 256) vmax = max(vmax, (uint32_t)(uniq[e] & vmask));
+    for (int o = 32; o > 0; o >>= 1) vmax = max(vmax, (uint32_t)__shfl_xor((int)vmax, o, 64));
+    if ((tid & 63) == 0) red[tid >> 6] = vmax;
+    for (int w = tid; w < NODE_WORDS; w += 256) bm[w] = 0u;
+    __syncthreads();
+    vmax = max(max(red[0], red[1]), max(red[2], red[3]));
+    const uint32_t nw = ((vmax - base) >> 5) + 1;
+    if (nw > (uint32_t)NODE_WORDS) {
+        for (int64_t e = e0 + tid; e < e1; e += 256) {
+            const uint64_t sk = uniq[e];
+            const uint32_t u = (uint32_t)(sk >> nb), v = (uint32_t)(sk & vmask);
+            if (e == 0 || (uint32_t)(uniq[e - 1] >> nb) != u) atomicOr(&bits[u >> 5], 1u << (u & 31));
+            atomicOr(&bits[v >> 5], 1u << (v & 31));
+        }
+        return;
+    }
+    for (int64_t e = e0 + tid; e < e1; e += 256) {
+        const uint64_t sk = uniq[e];
+        const uint32_t u = (uint32_t)(sk >> nb) - base, v = (uint32_t)(sk & vmask) - base;
+        if (e == 0 || (uint32_t)(uniq[e - 1] >> nb) != u + base) atomicOr(&bm[u >> 5], 1u << (u & 31));
+        atomicOr(&bm[v >> 5], 1u << (v & 31));
+    }
+    __syncthreads();
+    for (uint32_t w = tid; w < nw; w += 256) {
+        const uint32_t b = bm[w];
+        if (b) atomicOr(&bits[(base >> 5) + w], b);
+    }
+}
+
+hipError_t launch_mark_nodes(int64_t E, const uint32_t* dE, const uint64_t* uniq, int nb, uint32_t* bits,
+                             hipStream_t s) {
     if (E == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_mark_nodes, dim3((unsigned)((E + 255) / 256)), dim3(256), 0, s, E, uniq, nb, bits);
+    if (getenv("CTG_NODES_ATOMIC"))   // A/B: one global atomic per edge
+        hipLaunchKernelGGL(k_mark_nodes, dim3((unsigned)((E + 255) / 256)), dim3(256), 0, s, E, dE, uniq, nb, bits);
+    else
+        hipLaunchKernelGGL(k_mark_nodes_win, dim3((unsigned)((E + NODE_CHUNK - 1) / NODE_CHUNK)), dim3(256), 0, s,
+                           E, dE, uniq, nb, bits);
     return hipGetLastError();
 }
 hipError_t launch_popc_words(int64_t W, const uint32_t* bits, uint32_t* cnt, hipStream_t s) {
@@ -297,8 +366,9 @@ hipError_t launch_popc_words(int64_t W, const uint32_t* bits, uint32_t* cnt, hip
     return hipGetLastError();
 }
 hipError_t launch_bits_to_nodes(int64_t W, const uint32_t* bits, const uint32_t* off, uint64_t* nodes,
-                                hipStream_t s) {
-    hipLaunchKernelGGL(k_bits_to_nodes, dim3((unsigned)((W + 255) / 256)), dim3(256), 0, s, W, bits, off, nodes);
+                                const uint32_t* cnt, uint32_t* dN, hipStream_t s) {
+    hipLaunchKernelGGL(k_bits_to_nodes, dim3((unsigned)((W + 255) / 256)), dim3(256), 0, s, W, bits, off, nodes, cnt,
+                       dN);
     return hipGetLastError();
 }
 
@@ -382,24 +452,26 @@ hipError_t launch_max_pairs(int64_t n, const uint64_t* uv, unsigned long long* o
     hipLaunchKernelGGL(k_max_pairs, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, n, uv, out);
     return hipGetLastError();
 }
-hipError_t launch_reduce(int64_t E, const uint64_t* uniq, const uint32_t* runs, const uint32_t* offs,
-                         const uint32_t* perm, const RecordBuf& R, int wide, int stats, int nb, int need_adj,
-                         int ignore_label, double scale, double offset, const ReduceOut& O, hipStream_t s) {
+hipError_t launch_reduce(int64_t E, const uint32_t* dE, const uint64_t* uniq, const uint32_t* runs,
+                         const uint32_t* offs, const uint32_t* perm, const RecordBuf& R, int wide, int stats, int nb,
+                         int need_adj, int ignore_label, double scale, double offset, const ReduceOut& O,
+                         hipStream_t s) {
     if (E == 0) return hipSuccess;
     dim3 g((unsigned)((E + 255) / 256)), b(256);
     if (wide) {
-        if (stats) hipLaunchKernelGGL((k_reduce_edges<true, true>), g, b, 0, s, E, uniq, runs, offs, perm, R, nb, need_adj, ignore_label, scale, offset, O);
-        else hipLaunchKernelGGL((k_reduce_edges<true, false>), g, b, 0, s, E, uniq, runs, offs, perm, R, nb, need_adj, ignore_label, scale, offset, O);
+        if (stats) hipLaunchKernelGGL((k_reduce_edges<true, true>), g, b, 0, s, E, dE, uniq, runs, offs, perm, R, nb, need_adj, ignore_label, scale, offset, O);
+        else hipLaunchKernelGGL((k_reduce_edges<true, false>), g, b, 0, s, E, dE, uniq, runs, offs, perm, R, nb, need_adj, ignore_label, scale, offset, O);
     } else {
-        if (stats) hipLaunchKernelGGL((k_reduce_edges<false, true>), g, b, 0, s, E, uniq, runs, offs, perm, R, nb, need_adj, ignore_label, scale, offset, O);
-        else hipLaunchKernelGGL((k_reduce_edges<false, false>), g, b, 0, s, E, uniq, runs, offs, perm, R, nb, need_adj, ignore_label, scale, offset, O);
+        if (stats) hipLaunchKernelGGL((k_reduce_edges<false, true>), g, b, 0, s, E, dE, uniq, runs, offs, perm, R, nb, need_adj, ignore_label, scale, offset, O);
+        else hipLaunchKernelGGL((k_reduce_edges<false, false>), g, b, 0, s, E, dE, uniq, runs, offs, perm, R, nb, need_adj, ignore_label, scale, offset, O);
     }
     return hipGetLastError();
 }
-hipError_t launch_compact(int64_t E, const uint32_t* keep, const uint32_t* pos, const ReduceOut& in,
-                          const ReduceOut& out, hipStream_t s) {
+hipError_t launch_compact(int64_t E, const uint32_t* dE, const uint32_t* keep, const uint32_t* pos,
+                          const ReduceOut& in, const ReduceOut& out, uint32_t* dkept, hipStream_t s) {
     if (E == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_compact, dim3((unsigned)((E + 255) / 256)), dim3(256), 0, s, E, keep, pos, in, out);
+    hipLaunchKernelGGL(k_compact, dim3((unsigned)((E + 255) / 256)), dim3(256), 0, s, E, dE, keep, pos, in, out,
+                       dkept);
     return hipGetLastError();
 }
 hipError_t launch_endpoints(int64_t E, const uint64_t* uniq, int nb, uint32_t* out, hipStream_t s) {

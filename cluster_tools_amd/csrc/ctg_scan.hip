@@ -133,17 +133,21 @@ __device__ void table_flush(Table& T, RecordBuf R, Counters* C) {
         const unsigned long long base = T.base;
         for (uint32_t r = tid; r < n; r += SCAN_THREADS) {
             const int e = T.compact[r];
-            if (base + r < (unsigned long long)R.cap) {
-                R.key[base + r] = T.key[e];
-                if (MODE != MODE_GRAPH) R.sums[base + r] = make_double2(T.sum[e], T.sq[e]);
-            }
+            if (base + r < (unsigned long long)R.cap) R.key[base + r] = T.key[e];
         }
         if (MODE != MODE_GRAPH) {
-            // coalesced copy of the 24-word rows
-            for (uint32_t f = tid; f < n * NREC_WORDS; f += SCAN_THREADS) {
-                const uint32_t r = f / NREC_WORDS, j = f - r * NREC_WORDS;
-                if (base + r < (unsigned long long)R.cap)
-                    R.hist[(base + r) * NREC_WORDS + j] = T.w[T.compact[r]][j];
+            // coalesced copy into the 128-byte record bodies
+            for (uint32_t f = tid; f < n * NREC_STRIDE; f += SCAN_THREADS) {
+                const uint32_t r = f / NREC_STRIDE, j = f % NREC_STRIDE;
+                const int e = T.compact[r];
+                uint32_t val = 0u;
+                if (j < NREC_OFF) {
+                    const uint32_t* sw = reinterpret_cast<const uint32_t*>(j < 2 ? &T.sum[e] : &T.sq[e]);
+                    val = sw[j & 1];
+                } else if (j < NREC_OFF + NREC_WORDS) {
+                    val = T.w[e][j - NREC_OFF];
+                }
+                if (base + r < (unsigned long long)R.cap) R.hist[(base + r) * NREC_STRIDE + j] = val;
             }
         }
         lds_barrier();
@@ -170,16 +174,18 @@ __device__ __noinline__ void emit_direct(RecordBuf R, Counters* C, uint64_t key,
     if (i >= (unsigned long long)R.cap) return;
     R.key[i] = key;
     if (!with_stats) return;
-    R.sums[i] = make_double2(s, q);
+    uint32_t* b = R.hist + i * NREC_STRIDE;
+    reinterpret_cast<double2*>(b)[0] = make_double2(s, q);
     for (int j = 0; j < HWORDS; ++j) {
         uint32_t v = 0;
         if (sa >= 0 && (sa >> 1) == j) v += 1u << ((sa & 1) * 16);
         if (sb >= 0 && (sb >> 1) == j) v += 1u << ((sb & 1) * 16);
-        R.hist[i * NREC_WORDS + j] = v;
+        b[NREC_OFF + j] = v;
     }
-    R.hist[i * NREC_WORDS + 21] = cnt_flag;
-    R.hist[i * NREC_WORDS + 22] = mn;
-    R.hist[i * NREC_WORDS + 23] = mx;
+    b[NREC_OFF + 21] = cnt_flag;
+    b[NREC_OFF + 22] = mn;
+    b[NREC_OFF + 23] = mx;
+    for (int j = NREC_OFF + NREC_WORDS; j < NREC_STRIDE; ++j) b[j] = 0u;
 }
 
 template <typename DataT>

@@ -1,5 +1,3 @@
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-timeout -k 10 200 python tools/ablate2.py v5c@0@4 v5c@0@8 v5c@64@4 v5c@128@4 v5c@32@4 2>&1 | grep -v amdgpu.ids
-export CTG_CHECK_PLANES=4
-timeout -k 10 200 bash tools/sq_passes.sh sq5 && python tools/pmc_table.py gpurun_out/sq5
+timeout -k 10 200 bash tools/sq_passes.sh sq6 "FETCH_SIZE" "WRITE_SIZE" "SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_FLAT SQ_INST_CYCLES_VMEM_RD SQ_ACTIVE_INST_FLAT SQ_WAIT_INST_ANY" && python tools/pmc_table.py gpurun_out/sq6 k_reduce_edges
