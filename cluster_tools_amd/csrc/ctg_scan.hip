@@ -47,6 +47,11 @@ enum { MODE_GRAPH = 0, MODE_BOUNDARY = 1, MODE_AFFINITY = 2 };
 constexpr int ROWS = CTG_ROWS;                            // y rows per wave, held in registers
 constexpr int WAVES = SCAN_THREADS / WAVE;                // 8
 constexpr int WG_ROWS = ROWS * WAVES;                     // tile y extent
+#ifndef CTG_NPER
+#define CTG_NPER 2
+#endif
+constexpr int NPER = CTG_NPER;                            // staged entries folded per lane
+constexpr int STAGE_CAP = WAVE * NPER;                    // stage entries per wave
 constexpr uint32_t CNT_HARD = 65535u;                     // u16 histogram slots: count bound
 constexpr uint32_t CNT_SOFT = 40000u;                     // ask for a flush past this count
 constexpr uint32_t FILL_SOFT = TABLE_CAP * 3 / 8;         // ask for a flush past this many keys
@@ -227,24 +232,11 @@ __device__ __forceinline__ void hist_add2(Table& T, int e, int sa, int sb) {
     if (!same) atomicAdd(&T.w[e][sb >> 1], ib);
 }
 
-// claim or find the slot of key (u,v); -1 when the table is full
-__device__ __forceinline__ int table_slot(Table& T, uint32_t u, uint32_t v, bool& need) {
-    const uint64_t key = ((uint64_t)u << 32) | v;
-    const uint32_t h = home_bucket(u, v);
-    const uint4 b01 = *reinterpret_cast<const uint4*>(&T.key[h]);
-    const uint4 b23 = *reinterpret_cast<const uint4*>(&T.key[h + 2]);
-    const uint64_t kk[4] = {((uint64_t)b01.y << 32) | b01.x, ((uint64_t)b01.w << 32) | b01.z,
-                            ((uint64_t)b23.y << 32) | b23.x, ((uint64_t)b23.w << 32) | b23.z};
-    int s = -1, empty = -1;
-#pragma unroll
-    for (int j = 3; j >= 0; --j) {
-        s = kk[j] == key ? (int)h + j : s;
-        empty = kk[j] == EMPTY_KEY ? j : empty;
-    }
-    if (s >= 0) return s;
-    // not in the home bucket: claim its first empty slot (probe order is linear
-    // from the bucket start, so the key cannot sit beyond an empty slot); a
-    // lost race or a full bucket walks on
+// probe/insert past the home bucket (a key missing from its bucket); -1 when
+// the table is too full
+__device__ __noinline__ int table_insert(Table& T, uint32_t h, int empty, uint64_t key, bool& need) {
+    // probe order is linear from the bucket start, so the key cannot sit
+    // beyond an empty slot; a lost race or a full bucket walks on
     uint32_t p = h + (empty >= 0 ? (uint32_t)empty : 4u);
 #pragma unroll 1
     for (int i = 0; i < 64; ++i, p = (p + 1) & (TABLE_CAP - 1)) {
@@ -263,21 +255,29 @@ __device__ __forceinline__ int table_slot(Table& T, uint32_t u, uint32_t v, bool
     return -1;
 }
 
-// Fold the wave's nb staged entries (one per lane) into the LDS edge table.
+// slot of key in its 4-slot home bucket (b01, b23 = the bucket's keys), -1 if
+// absent; `empty` = first empty slot of the bucket or -1
+__device__ __forceinline__ int bucket_match(const uint4& b01, const uint4& b23, uint32_t h, uint64_t key,
+                                            int& empty) {
+    const uint64_t kk[4] = {((uint64_t)b01.y << 32) | b01.x, ((uint64_t)b01.w << 32) | b01.z,
+                            ((uint64_t)b23.y << 32) | b23.x, ((uint64_t)b23.w << 32) | b23.z};
+    int s = -1;
+    empty = -1;
+#pragma unroll
+    for (int j = 3; j >= 0; --j) {
+        s = kk[j] == key ? (int)h + j : s;
+        empty = kk[j] == EMPTY_KEY ? j : empty;
+    }
+    return s;
+}
+
+// statistics of one staged entry into table slot s (s < 0: direct record)
 template <int MODE, bool FAST40, typename StageT>
-__device__ __forceinline__ void fold_batch(Table& T, const StageT* __restrict__ stage, int nb, int lane, RecordBuf R,
-                                           Counters* C, double scale, double offset, bool& need, int ablate) {
+__device__ __forceinline__ void fold_stats(Table& T, const StageT& e, int s, RecordBuf R, Counters* C, double scale,
+                                           double offset, bool& need, int ablate) {
     constexpr bool BND = MODE == MODE_BOUNDARY;
     constexpr bool AFF = MODE == MODE_AFFINITY;
-    if (lane >= nb) return;
-    const StageT e = stage[lane];
-    if (ablate & 32) {   // diagnostic: staging only, no fold
-        if (e.x == 0x12345u && e.y == 0x6789u) atomicAdd(&C->pad[1], 1ull);
-        return;
-    }
-    const uint32_t u = e.x, v = e.y;
-    const uint64_t key = ((uint64_t)u << 32) | v;
-    const int s = table_slot(T, u, v, need);
+    const uint64_t key = ((uint64_t)e.x << 32) | e.y;
     if constexpr (MODE == MODE_GRAPH) {
         if (s < 0) emit_direct(R, C, key, 0u, -1, -1, 0.0, 0.0, 0u, 0u, false);
         return;
@@ -324,6 +324,53 @@ __device__ __forceinline__ void fold_batch(Table& T, const StageT* __restrict__ 
     }
 }
 
+// Fold the wave's nb staged entries into the LDS edge table: NPER entries per
+// lane (lane, lane+64, ...), their stage reads and home-bucket reads issued
+// together so the LDS round trips of the entries overlap.
+template <int MODE, bool FAST40, typename StageT, int NPER>
+__device__ __forceinline__ void fold_batch(Table& T, const StageT* __restrict__ stage, int nb, int lane, RecordBuf R,
+                                           Counters* C, double scale, double offset, bool& need, int ablate) {
+    StageT e[NPER];
+    uint32_t h[NPER];
+    uint4 b01[NPER], b23[NPER];
+#pragma unroll
+    for (int i = 0; i < NPER; ++i) e[i] = stage[lane + WAVE * i];   // past nb: stale, ignored
+    if (ablate & 32) {   // diagnostic: staging only, no fold
+#pragma unroll
+        for (int i = 0; i < NPER; ++i)
+            if (lane + WAVE * i < nb && e[i].x == 0x12345u && e[i].y == 0x6789u) atomicAdd(&C->pad[1], 1ull);
+        return;
+    }
+#pragma unroll
+    for (int i = 0; i < NPER; ++i) {
+        h[i] = home_bucket(e[i].x, e[i].y);
+        b01[i] = *reinterpret_cast<const uint4*>(&T.key[h[i]]);
+        b23[i] = *reinterpret_cast<const uint4*>(&T.key[h[i] + 2]);
+    }
+#pragma unroll
+    for (int i = 0; i < NPER; ++i) {
+        if (lane + WAVE * i >= nb) continue;
+        const uint64_t key = ((uint64_t)e[i].x << 32) | e[i].y;
+        int empty;
+        int s = bucket_match(b01[i], b23[i], h[i], key, empty);
+        if (s < 0) {
+            // not in the home bucket: claim its first empty slot with one CAS
+            if (empty >= 0) {
+                const uint64_t old = atomicCAS((unsigned long long*)&T.key[h[i] + empty],
+                                               (unsigned long long)EMPTY_KEY, (unsigned long long)key);
+                if (old == EMPTY_KEY) {
+                    if (atomicAdd(&T.used, 1u) + 1u > FILL_SOFT) need = true;
+                    s = (int)h[i] + empty;
+                } else if (old == key) {
+                    s = (int)h[i] + empty;
+                }
+            }
+            if (s < 0) s = table_insert(T, h[i], empty, key, need);
+        }
+        fold_stats<MODE, FAST40, StageT>(T, e[i], s, R, C, scale, offset, need, ablate);
+    }
+}
+
 // x-neighbour of every lane: lane i gets lane i+1 (DPP wave_shl:1), lane 63
 // gets `edge` (the x-halo value)
 __device__ __forceinline__ uint32_t shl1(uint32_t v, uint32_t edge) {
@@ -337,7 +384,7 @@ __global__ __launch_bounds__(SCAN_THREADS, 4) void k_face_scan(ScanParams P, Rec
     constexpr bool STATS = MODE != MODE_GRAPH;
     using StageT = typename std::conditional<STATS, uint4, uint2>::type;
     __shared__ Table T;
-    __shared__ StageT stage_all[WAVES][WAVE];
+    __shared__ StageT stage_all[WAVES][STAGE_CAP];
     __shared__ uint32_t needw[2][WAVES];   // per-wave flush requests, alternating by check parity
     const int tid = threadIdx.x;
     const int lane = tid & (WAVE - 1);
@@ -422,7 +469,7 @@ __global__ __launch_bounds__(SCAN_THREADS, 4) void k_face_scan(ScanParams P, Rec
     int nbuf = 0;   // staged entries (wave-uniform)
     auto flush_stage = [&]() {
         if (nbuf) {
-            fold_batch<MODE, FAST40, StageT>(T, stage, nbuf, lane, R, C, scale, offset, need, ablate);
+            fold_batch<MODE, FAST40, StageT, NPER>(T, stage, nbuf, lane, R, C, scale, offset, need, ablate);
             nbuf = 0;
         }
     };
@@ -431,7 +478,7 @@ __global__ __launch_bounds__(SCAN_THREADS, 4) void k_face_scan(ScanParams P, Rec
         const uint64_t m = __ballot(act);
         if (m == 0) return;
         const int k = __popcll(m);
-        if (nbuf + k > WAVE) flush_stage();
+        if (nbuf + k > STAGE_CAP) flush_stage();
         const int rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
         if (act) {
             if constexpr (STATS) stage[nbuf + rank] = make_uint4(min(a, b), max(a, b), za, zb);
