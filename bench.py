@@ -7,11 +7,20 @@ resident synthetic volume: face scan (labels uint64 + float32 boundary map in
 HBM) -> per-tile edge records -> radix sort -> per-edge reduction -> sorted
 (E,2) edge table, node list and (E,10) float64 feature table in HBM.
 
-N=1: BASELINE.json configs[1], 512^3 Voronoi supervoxels (cell 10, ~1e6
-edges) + boundary map.  N>1 (torch.distributed.run, one rank per GPU): weak
-scaling, each rank owns a 512^3 z-slab of a (512N)x512x512 volume (+1 halo
-plane), builds its partial edge table and the ranks combine them over RCCL
-(cluster_tools_amd/dist.py).
+Default (``--config 1``): BASELINE.json configs[1], 512^3 Voronoi supervoxels
+(cell 10, ~1e6 edges) + boundary map per GPU.  N>1 (torch.distributed.run, one
+rank per GPU): weak scaling, each rank owns a 512^3 z-slab of a (512N)x512x512
+volume (+1 halo plane), builds its partial edge table and the ranks combine
+them over RCCL (cluster_tools_amd/dist.py).
+
+The other BASELINE configs are extra lines (``--config``), not the driver's
+bench line:
+  2    configs[2]: 2048^3 boundary map (cell 16), strong scaling: the fixed
+       volume is z-sharded over the ranks (2048/N planes each + 1 halo plane)
+  3    configs[3]: 1024^3, 3-channel nearest-neighbour affinities (N=1)
+  3lr  configs[3]: 1024^3, 12-channel long-range affinities (N=1)
+  4    configs[4]: 1024^3 high fragmentation (cell 5, ~5e7 edges), strong
+       scaling like config 2
 """
 from __future__ import annotations
 
@@ -30,13 +39,24 @@ HBM_PEAK_GBS = 8000.0          # MI355X HBM3E peak, GB/s (MI355X_MICROARCH.md)
 EDGE_BYTES = 96                # 16 B (u,v) + 10 x float64 features
 
 
+# BASELINE.json configs -> (cube edge, cell size, offsets or None, scaling, label)
+WORKLOADS = {
+    '1': (512, 10, None, 'weak', 'BASELINE configs[1]: %d^3 per GPU, cell %d, boundary map'),
+    '2': (2048, 16, None, 'strong', 'BASELINE configs[2]: %d^3 boundary map, cell %d, z-slab sharded'),
+    '3': (1024, 10, 'nn', 'strong', 'BASELINE configs[3]: %d^3, cell %d, 3-channel nearest-neighbour affinities'),
+    '3lr': (1024, 10, 'lr', 'strong', 'BASELINE configs[3]: %d^3, cell %d, 12-channel long-range affinities'),
+    '4': (1024, 5, None, 'strong', 'BASELINE configs[4]: %d^3 high fragmentation, cell %d, boundary map'),
+}
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument('--gpus', type=int, default=1)
     p.add_argument('--steps', type=int, default=10)
     p.add_argument('--warmup', type=int, default=3)
-    p.add_argument('--size', type=int, default=512, help='per-GPU cube edge (voxels)')
-    p.add_argument('--cell', type=int, default=10)
+    p.add_argument('--config', default='1', choices=sorted(WORKLOADS))
+    p.add_argument('--size', type=int, default=None, help='cube edge (voxels; per GPU for weak scaling)')
+    p.add_argument('--cell', type=int, default=None)
     p.add_argument('--seed', type=int, default=0)
     p.add_argument('--cpu-baseline-planes', type=int, default=96,
                    help='z-planes of the per-GPU volume timed with the C oracle (0 = skip)')
@@ -92,21 +112,41 @@ def main():
     from cluster_tools_amd import _lib
 
     _lib.init_device(local)
-    S = args.size
-    shape = (S, S, S)
-    gshape = (S * world, S, S)
+    S0, cell0, aff, scaling, label = WORKLOADS[args.config]
+    S = args.size or S0
+    cell = args.cell or cell0
+    if aff and world > 1:
+        raise SystemExit('affinity workloads are single-GPU lines (--gpus 1)')
+    if scaling == 'weak':
+        Zr = S                                 # owned planes per rank
+        gshape = (S * world, S, S)
+    else:
+        if S % world:
+            raise SystemExit('--size must be divisible by the number of ranks')
+        Zr = S // world
+        gshape = (S, S, S)
     halo = 1 if rank > 0 else 0
-    # rank r owns z in [r*S, (r+1)*S) and reads the plane below as halo
-    lab, bnd = rag.synth_volume((S + halo, S, S), cell=args.cell, seed=args.seed, z_offset=rank * S - halo,
+    # rank r owns z in [r*Zr, (r+1)*Zr) and reads the plane below as halo
+    lab, bnd = rag.synth_volume((Zr + halo, S, S), cell=cell, seed=args.seed, z_offset=rank * Zr - halo,
                                 global_shape=gshape)
-    torch.cuda.synchronize()
     own = (halo, 0, 0)
+    offsets = None
+    data = bnd
+    n_ch = 1
+    if aff:
+        from cluster_tools_amd import synthetic
+        offsets = synthetic.NN_OFFSETS if aff == 'nn' else synthetic.LR_OFFSETS
+        data = rag.synth_affinities(bnd, offsets)
+        n_ch = len(offsets)
+        del bnd
+        bnd = None
+    torch.cuda.synchronize()
 
     if world > 1:
         from cluster_tools_amd import dist as cdist
-        step_fn = lambda: cdist.rag_features_distributed(lab, bnd, own_begin=own)  # noqa: E731
+        step_fn = lambda: cdist.rag_features_distributed(lab, data, offsets=offsets, own_begin=own)  # noqa: E731
     else:
-        step_fn = lambda: rag.rag_features_handle(lab, bnd, own_begin=own)  # noqa: E731
+        step_fn = lambda: rag.rag_features_handle(lab, data, offsets=offsets, own_begin=own)  # noqa: E731
 
     res = None
     for _ in range(args.warmup):
@@ -139,7 +179,7 @@ def main():
     n_rec, n_direct = res.info()
     timings = rag.last_timings()
 
-    V = S ** 3                                # owned voxels per rank
+    V = Zr * S * S                            # owned voxels per rank
     total_vox = V * world
     ms_step = elapsed / args.steps * 1e3
     value = total_vox / (elapsed / args.steps) / 1e9
@@ -150,23 +190,25 @@ def main():
         n_edges = int(te.item())
 
     # roofline of the dominant kernel (face scan): algorithmic bytes per launch
-    # = voxels it scans x (8 B label + 4 B boundary), halo plane excluded
+    # = voxels it scans x (8 B label + 4 B per channel), halo plane excluded
     scan_avg_ms = float(np.mean(scan_ms))
-    scan_bytes = V * 12
+    vox_bytes = 8 + 4 * n_ch
+    scan_bytes = V * vox_bytes
     achieved = scan_bytes / (scan_avg_ms * 1e-3) / 1e9
-    traffic, traffic_src = pmc_traffic_per_launch()
-    step_bytes = total_vox * 12 + n_edges * EDGE_BYTES
+    traffic, traffic_src = pmc_traffic_per_launch() if args.config == '1' else (None, None)
+    step_bytes = total_vox * vox_bytes + n_edges * EDGE_BYTES
 
     line = None
     if rank == 0:
         cpu = None
-        if not args.no_cpu_baseline and args.cpu_baseline_planes > 0 and world == 1:
+        if not args.no_cpu_baseline and args.cpu_baseline_planes > 0 and world == 1 and args.config == '1':
             v, info = cpu_baseline(lab, bnd, min(args.cpu_baseline_planes, S))
             cpu = {'value': round(v, 6), 'unit': 'Gvoxels/s', 'cores': 1, 'kind': 'port',
                    'sample': info['sample'] + ', %.2f s, oracle/ctg_oracle.c scalar C restatement '
                                               '(nifty reference not present on this host)' % info['seconds']}
         line = {
-            'metric': 'Gvoxels/s RAG+edge features (boundary map, uint64 labels, float32)',
+            'metric': 'Gvoxels/s RAG+edge features (%s, uint64 labels, float32)'
+                      % ('boundary map' if not aff else '%d-channel affinity map' % n_ch),
             'value': round(value, 4),
             'unit': 'Gvoxels/s',
             'n_gpus': world,
@@ -174,11 +216,11 @@ def main():
             'warmup': args.warmup,
             'ms_per_step': round(ms_step, 4),
             'higher_is_better': True,
-            'scaling': 'weak',
+            'scaling': scaling,
             'vs_baseline': None,
             'dtype': 'u64 labels / f32 samples / f64 stats',
             'data': 'synthetic (jittered-grid Voronoi supervoxels + boundary map, generated in HBM)',
-            'config': {'workload': 'BASELINE configs[1]: %d^3 per GPU, cell %d, boundary map' % (S, args.cell),
+            'config': {'workload': label % (S, cell),
                        'volume': list(gshape), 'edges': n_edges, 'parallelism': 'z-slab x%d' % world},
             'roofline': {'bound': 'hbm', 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                          'frac': round(achieved / HBM_PEAK_GBS, 4),

@@ -30,8 +30,8 @@
 // record instead (its sum / min / max are already in the table entry: records
 // of one key are additive, so splitting a face's contributions between two
 // records is exact).  Table fill and count pressure only set a per-lane
-// "need flush" flag; the workgroup decides on a flush every check_planes
-// planes with one __syncthreads_or.
+// "need flush" flag; the wave then raises the workgroup's flush request, which
+// every wave polls after each fold batch and plane (see k_face_scan).
 #include <type_traits>
 
 #include "ctg_internal.h"
@@ -54,7 +54,10 @@ constexpr int NPER = CTG_NPER;                            // staged entries fold
 constexpr int STAGE_CAP = WAVE * NPER;                    // stage entries per wave
 constexpr uint32_t CNT_HARD = 65535u;                     // u16 histogram slots: count bound
 constexpr uint32_t CNT_SOFT = 40000u;                     // ask for a flush past this count
-constexpr uint32_t FILL_SOFT = TABLE_CAP * 3 / 8;         // ask for a flush past this many keys
+#ifndef CTG_FILL_SOFT
+#define CTG_FILL_SOFT (TABLE_CAP / 2)
+#endif
+constexpr uint32_t FILL_SOFT = CTG_FILL_SOFT;             // request a flush past this many keys
 constexpr uint32_t MARK_ADJ = 0xFFFFFFFFu;                // stage entry: nearest-neighbour face, no sample
 constexpr uint32_t MARK_ONE = 0xFFFFFFFEu;                // stage entry: one affinity sample in .z
 
@@ -68,6 +71,8 @@ struct __align__(16) Table {
     uint16_t compact[TABLE_CAP];
     uint32_t wave_cnt[WAVES];
     uint32_t used;
+    uint32_t flush_req;   // a wave asked for a flush; every wave joins at its next poll
+    uint32_t live;        // waves still walking their planes
     uint32_t ncompact;
     unsigned long long base;
     unsigned long long maxv;
@@ -103,7 +108,7 @@ __device__ __forceinline__ void lds_barrier() {
 }
 
 template <int MODE>
-__device__ void table_flush(Table& T, RecordBuf R, Counters* C) {
+__device__ __noinline__ void table_flush(Table& T, RecordBuf R, Counters* C) {
     static_assert(TABLE_CAP == SCAN_THREADS, "one table entry per thread in the flush");
     lds_barrier();
     const int tid = threadIdx.x;
@@ -163,6 +168,7 @@ __device__ void table_flush(Table& T, RecordBuf R, Counters* C) {
         T.used = 0;
         T.ncompact = 0;
         T.maxv = 0;
+        T.flush_req = 0;
     }
     lds_barrier();
 }
@@ -233,8 +239,11 @@ __device__ __forceinline__ void hist_add2(Table& T, int e, int sa, int sb) {
 }
 
 // probe/insert past the home bucket (a key missing from its bucket); -1 when
-// the table is too full
-__device__ __noinline__ int table_insert(Table& T, uint32_t h, int empty, uint64_t key, bool& need) {
+// the table is too full.  INSERT_OVER is or-ed into the slot when this insert
+// took the table past FILL_SOFT (a flag, not a reference: a bool& argument of
+// an out-of-line call would live in scratch memory).
+constexpr int INSERT_OVER = 0x10000;
+__device__ __noinline__ int table_insert(Table& T, uint32_t h, int empty, uint64_t key) {
     // probe order is linear from the bucket start, so the key cannot sit
     // beyond an empty slot; a lost race or a full bucket walks on
     uint32_t p = h + (empty >= 0 ? (uint32_t)empty : 4u);
@@ -245,13 +254,9 @@ __device__ __noinline__ int table_insert(Table& T, uint32_t h, int empty, uint64
         if (cur != EMPTY_KEY) continue;
         const uint64_t old =
             atomicCAS((unsigned long long*)&T.key[p], (unsigned long long)EMPTY_KEY, (unsigned long long)key);
-        if (old == EMPTY_KEY) {
-            if (atomicAdd(&T.used, 1u) + 1u > FILL_SOFT) need = true;
-            return (int)p;
-        }
+        if (old == EMPTY_KEY) return (int)p | (atomicAdd(&T.used, 1u) + 1u > FILL_SOFT ? INSERT_OVER : 0);
         if (old == key) return (int)p;
     }
-    need = true;
     return -1;
 }
 
@@ -365,7 +370,11 @@ __device__ __forceinline__ void fold_batch(Table& T, const StageT* __restrict__ 
                     s = (int)h[i] + empty;
                 }
             }
-            if (s < 0) s = table_insert(T, h[i], empty, key, need);
+            if (s < 0) {
+                s = table_insert(T, h[i], empty, key);
+                need |= s < 0 || (s & INSERT_OVER) != 0;
+                s = s < 0 ? s : (s & (INSERT_OVER - 1));
+            }
         }
         fold_stats<MODE, FAST40, StageT>(T, e[i], s, R, C, scale, offset, need, ablate);
     }
@@ -385,7 +394,6 @@ __global__ __launch_bounds__(SCAN_THREADS, 4) void k_face_scan(ScanParams P, Rec
     using StageT = typename std::conditional<STATS, uint4, uint2>::type;
     __shared__ Table T;
     __shared__ StageT stage_all[WAVES][STAGE_CAP];
-    __shared__ uint32_t needw[2][WAVES];   // per-wave flush requests, alternating by check parity
     const int tid = threadIdx.x;
     const int lane = tid & (WAVE - 1);
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -395,6 +403,8 @@ __global__ __launch_bounds__(SCAN_THREADS, 4) void k_face_scan(ScanParams P, Rec
         T.used = 0;
         T.ncompact = 0;
         T.maxv = 0;
+        T.flush_req = 0;
+        T.live = WAVES;
     }
     __syncthreads();
 
@@ -465,12 +475,28 @@ __global__ __launch_bounds__(SCAN_THREADS, 4) void k_face_scan(ScanParams P, Rec
         }
     };
 
+    // Flushes on demand: a wave whose fold found the table past FILL_SOFT (or
+    // an entry near its count bound) raises T.flush_req; every wave polls it
+    // after each fold batch and at each plane end, and all eight then run
+    // table_flush together (its barriers are the only workgroup barriers).
+    // Waves done with their planes keep polling until the last one is done,
+    // so a request never waits for a wave that has left the loop.
     bool need = false;
     int nbuf = 0;   // staged entries (wave-uniform)
+    auto poll = [&]() {
+        if (__ballot(need)) {
+            if (lane == 0) atomicOr(&T.flush_req, 1u);
+            need = false;
+        }
+        const uint32_t fr = (uint32_t)__builtin_amdgcn_readfirstlane(
+            (int)__hip_atomic_load(&T.flush_req, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+        if (fr) table_flush<MODE>(T, R, C);
+    };
     auto flush_stage = [&]() {
         if (nbuf) {
             fold_batch<MODE, FAST40, StageT, NPER>(T, stage, nbuf, lane, R, C, scale, offset, need, ablate);
             nbuf = 0;
+            poll();
         }
     };
     // append the active lanes of one site to the stage
@@ -487,14 +513,12 @@ __global__ __launch_bounds__(SCAN_THREADS, 4) void k_face_scan(ScanParams P, Rec
         nbuf += k;
     };
 
-    const int check = P.check_planes;
     if (z0 < z1) {
         load_plane(z0, Ln, Dc, XLn, XDc);
 #pragma unroll
         for (int r = 0; r <= ROWS; ++r) Lc[r] = narrow(Ln[r]);
         XLc = narrow(XLn);
     }
-    int since = 0, parity = 0;
     for (int z = z0; z < z1; ++z) {
         const bool hz = z + 1 < Z;
         if (hz) load_plane(z + 1, Ln, Dn, XLn, XDn);        // prefetch: in flight during x/y faces
@@ -554,22 +578,9 @@ __global__ __launch_bounds__(SCAN_THREADS, 4) void k_face_scan(ScanParams P, Rec
                 }
             }
         }
-        // flush decision: staged entries stay staged (raw faces are valid for
+        // staged entries stay staged across planes (raw faces are valid for
         // whatever table they are folded into later)
-        if (++since == check && z + 1 < z1) {
-            since = 0;
-            // every wave writes its request slot of this parity, so no reset is
-            // needed: the slots are rewritten two checks later, after every wave
-            // has passed the next check's barrier (and so has read these)
-            const bool wneed = __ballot(need) != 0;
-            if (lane == 0) needw[parity][wave] = wneed;
-            lds_barrier();
-            const uint4 n0 = *reinterpret_cast<const uint4*>(&needw[parity][0]);
-            const uint4 n1 = *reinterpret_cast<const uint4*>(&needw[parity][4]);
-            parity ^= 1;
-            if ((n0.x | n0.y | n0.z | n0.w | n1.x | n1.y | n1.z | n1.w) != 0u) table_flush<MODE>(T, R, C);
-            need = false;
-        }
+        poll();
 #pragma unroll
         for (int r = 0; r <= ROWS; ++r) {
             Lc[r] = narrow(Ln[r]);
@@ -580,6 +591,20 @@ __global__ __launch_bounds__(SCAN_THREADS, 4) void k_face_scan(ScanParams P, Rec
     }
     if (__ballot(ovf != 0) && lane == 0) atomicAdd(&C->label_overflow, 1ull);
     flush_stage();
+    poll();
+    if (lane == 0) atomicSub(&T.live, 1u);
+    while (true) {
+        const uint32_t fr = (uint32_t)__builtin_amdgcn_readfirstlane(
+            (int)__hip_atomic_load(&T.flush_req, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+        if (fr) {
+            table_flush<MODE>(T, R, C);
+            continue;
+        }
+        const uint32_t lv = (uint32_t)__builtin_amdgcn_readfirstlane(
+            (int)__hip_atomic_load(&T.live, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+        if (lv == 0) break;
+        __builtin_amdgcn_s_sleep(2);
+    }
     table_flush<MODE>(T, R, C);
 }
 
