@@ -1,6 +1,7 @@
 // C ABI of libctg.so (include/ctg.h): host orchestration of the face scan,
 // the record sort/reduction and the result handles.
 #include <hip/hip_runtime.h>
+#include <cstdlib>
 #include <cstring>
 #include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/device/device_run_length_encode.hpp>
@@ -35,6 +36,8 @@ hipError_t launch_mark_nodes(int64_t E, const uint32_t* dE, const uint64_t* uniq
 hipError_t launch_popc_words(int64_t W, const uint32_t* bits, uint32_t* cnt, hipStream_t s);
 hipError_t launch_bits_to_nodes(int64_t W, const uint32_t* bits, const uint32_t* off, uint64_t* nodes,
                                 const uint32_t* cnt, uint32_t* dN, hipStream_t s);
+hipError_t launch_build_adj_set(const uint64_t* edges, int64_t E, unsigned long long* set, uint32_t mask,
+                                hipStream_t s);
 hipError_t launch_find_edges(const uint64_t* ge, int64_t n, const uint64_t* q, int64_t m, int64_t* out,
                              hipStream_t s);
 hipError_t launch_synth(uint64_t* labels, float* boundary, const int64_t* shape, int64_t z_offset,
@@ -569,6 +572,60 @@ int ctg_rag_features(const void* labels, int label_bits, const void* data, int d
         const char* ab = getenv("CTG_ABLATE");
         P.ablate = ab ? atoi(ab) : 0;
     }
+
+    // Long-range affinity channels: a sample counts only if its
+    // (u,v) is a RAG edge.  Filtering in the scan (against the edge set of a
+    // graph-only pass) keeps the non-adjacent pairs - most long-range pairs -
+    // out of the edge tables and records.  Labels >= 2^32 skip it here: the
+    // dense-relabel path re-enters with 32-bit labels and filters there.
+    unsigned long long* adj_set = nullptr;
+    ctg_result* adj_graph = nullptr;
+    bool long_range = false;
+    for (int c = 0; c < P.n_channels; ++c)
+        long_range |= std::abs(P.offsets[c][0]) + std::abs(P.offsets[c][1]) + std::abs(P.offsets[c][2]) > 1;
+    if (long_range && !(flags & CTG_NO_ADJ_FILTER) && V > 0) {
+        rc = ctg_rag_features(dl, label_bits, nullptr, CTG_DATA_NONE, 0, nullptr, shape, own_begin, own_end, 0,
+                              hist_lo, hist_hi, 0, CTG_MEM_DEVICE, stream, &adj_graph);
+        if (rc) return rc;
+        uint64_t mx = 0;
+        if (adj_graph->n_edges > 0) {
+            // largest label of the sorted edge table: the v of some row; the
+            // max over all v equals the last node
+            CTG_CHECK(hipMemcpyAsync(&mx, adj_graph->nodes + adj_graph->n_nodes - 1, 8, hipMemcpyDeviceToHost, s));
+            CTG_CHECK(hipStreamSynchronize(s));
+        }
+        if ((mx >> 32) == 0) {
+            uint32_t cap = 1024;
+            while ((int64_t)cap < 2 * adj_graph->n_edges) cap *= 2;
+            adj_set = (unsigned long long*)dalloc((size_t)cap * 8);
+            if (!adj_set) {
+                ctg_free(adj_graph);
+                set_error("ctg_rag_features: out of memory (adjacency set)");
+                return CTG_ERR_NOMEM;
+            }
+            hipError_t e = launch_build_adj_set(adj_graph->edges, adj_graph->n_edges, adj_set, cap - 1, s);
+            if (e != hipSuccess) {
+                dfree(adj_set);
+                ctg_free(adj_graph);
+                set_error(std::string("ctg_rag_features: ") + hipGetErrorString(e));
+                return CTG_ERR_HIP;
+            }
+            P.adj_set = adj_set;
+            P.adj_mask = cap - 1;
+        }
+    }
+    struct AdjRelease {   // the set and its graph live until the scan is done
+        unsigned long long*& set;
+        ctg_result*& g;
+        hipStream_t s;
+        ~AdjRelease() {
+            if (set) {
+                hipStreamSynchronize(s);
+                dfree(set);
+            }
+            if (g) ctg_free(g);
+        }
+    } adj_release{adj_set, adj_graph, s};
 
     Ev ev{w, s};
     ev.mark(0);

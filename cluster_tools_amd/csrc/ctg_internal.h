@@ -90,6 +90,10 @@ struct ScanParams {
     int check_planes;          // planes between flush decisions
     int fast40;                // histogram range [0,1) x 40 bins: exact f32 binning
     int ablate;                // diagnostic: 8 loads only, 32 staging without fold
+    // long-range affinity channels: samples whose (u,v) is not in this open-
+    // addressing set of RAG edge keys ((u << 32) | v) are dropped in the scan
+    const unsigned long long* adj_set;
+    uint32_t adj_mask;         // set capacity - 1 (power of two)
 };
 
 struct Counters {               // device-side counters, zeroed per call

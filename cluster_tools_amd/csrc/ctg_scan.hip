@@ -380,6 +380,18 @@ __device__ __forceinline__ void fold_batch(Table& T, const StageT* __restrict__ 
     }
 }
 
+// membership of an edge key in the RAG edge set (linear probing, load <= 1/2)
+__device__ __forceinline__ bool adj_contains(const unsigned long long* __restrict__ set, uint32_t mask, uint64_t key) {
+    uint32_t h = hash_key(key) & mask;
+#pragma unroll 1
+    for (;;) {
+        const unsigned long long k = set[h];
+        if (k == key) return true;
+        if (k == EMPTY_KEY) return false;
+        h = (h + 1) & mask;
+    }
+}
+
 // x-neighbour of every lane: lane i gets lane i+1 (DPP wave_shl:1), lane 63
 // gets `edge` (the x-halo value)
 __device__ __forceinline__ uint32_t shl1(uint32_t v, uint32_t edge) {
@@ -562,7 +574,14 @@ __global__ __launch_bounds__(SCAN_THREADS, 4) void k_face_scan(ScanParams P, Rec
                                 lq = narrow(L[(int64_t)qz * sz + (int64_t)qy * X + qx]);
                                 av = load_val<DataT>(D, (int64_t)c * Z * sz + i);
                             }
-                            push(inq && lq != lc, lc, lq, __float_as_uint(av), MARK_ONE);
+                            bool act = inq && lq != lc;
+                            // long-range channel: only pairs that are RAG edges
+                            if (P.adj_set != nullptr && (abs(P.offsets[c][0]) + abs(P.offsets[c][1]) +
+                                                             abs(P.offsets[c][2])) > 1) {
+                                if (act) act = adj_contains(P.adj_set, P.adj_mask,
+                                                            ((uint64_t)min(lc, lq) << 32) | max(lc, lq));
+                            }
+                            push(act, lc, lq, __float_as_uint(av), MARK_ONE);
                         }
                     }
                 }
