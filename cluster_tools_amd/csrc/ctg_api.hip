@@ -566,11 +566,16 @@ int ctg_rag_features(const void* labels, int label_bits, const void* data, int d
         const int64_t cols = ((shape[2] + TILE_X - 1) / TILE_X) * ((shape[1] + rows - 1) / rows);
         int tz = 64;
         while (tz > 8 && cols * ((shape[0] + tz - 1) / tz) < 1024) tz /= 2;
+        if (const char* t = getenv("CTG_TILE_Z")) tz = std::max(1, atoi(t));
         P.tile_z = tz;
     }
     {
         const char* ab = getenv("CTG_ABLATE");
         P.ablate = ab ? atoi(ab) : 0;
+    }
+    {
+        const char* xr = getenv("CTG_XCD_REMAP");
+        P.xcd_remap = xr ? atoi(xr) : 1;
     }
 
     // Long-range affinity channels: a sample counts only if its

@@ -94,6 +94,8 @@ struct ScanParams {
     // addressing set of RAG edge keys ((u << 32) | v) are dropped in the scan
     const unsigned long long* adj_set;
     uint32_t adj_mask;         // set capacity - 1 (power of two)
+    int64_t ntiles[3];         // tiles along x, y, z (set by the launcher)
+    int xcd_remap;             // 1: XCD-contiguous tile order (see k_face_scan)
 };
 
 struct Counters {               // device-side counters, zeroed per call

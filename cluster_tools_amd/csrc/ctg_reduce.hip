@@ -60,8 +60,12 @@ __device__ __forceinline__ double qv5(int i) {
     return i == 0 ? 0.1 : i == 1 ? 0.25 : i == 2 ? 0.5 : i == 3 ? 0.75 : 0.9;
 }
 
-__device__ void vigra_quantiles(const uint32_t* __restrict__ hl, double count, double vmin, double vmax,
-                                double scale, double offset, double* __restrict__ out) {
+// HL: a pointer to the NSLOTS bins, or the thread's register array itself
+// (the bin walk is fully unrolled, so the array is never indexed dynamically
+// and stays in registers - no LDS copy, no scratch)
+template <typename HL>
+__device__ __forceinline__ void vigra_quantiles(const HL& hl, double count, double vmin, double vmax, double scale,
+                                                double offset, double* __restrict__ out) {
     const double inv = 1.0 / scale;
     int q = 0;
     double qc = count * qv5(0);
@@ -93,7 +97,7 @@ __device__ void vigra_quantiles(const uint32_t* __restrict__ hl, double count, d
     const double left = (double)hl[0], right = (double)hl[NSLOTS - 1];
     if (left > 0.0) gen(0.0, left);
     double cum = left;
-#pragma unroll 1
+#pragma unroll
     for (int k = 0; k < NBINS; ++k) {
         const uint32_t hk = hl[k + 1];
         if (hk > 0) {
@@ -223,16 +227,11 @@ __global__ __launch_bounds__(256) void k_reduce_edges(int64_t E, const uint32_t*
         double var = (sq - sum * mean) / c;
         if (var < 0.0) var = 0.0;
         const double vmin = (double)ord2f(mn), vmax = (double)ord2f(mx);
-        // the walk reads the bins back from this thread's LDS row
-        __shared__ uint32_t H[256][NSLOTS + 1];
-        uint32_t* hl = H[threadIdx.x];
-#pragma unroll
-        for (int j = 0; j < NSLOTS; ++j) hl[j] = h[j];
         o[0] = mean;
         o[1] = var;
         o[2] = vmin;
         o[3] = o[4] = o[5] = o[6] = o[7] = 0.0;
-        vigra_quantiles(hl, c, vmin, vmax, scale, offset, o + 3);
+        vigra_quantiles(h, c, vmin, vmax, scale, offset, o + 3);
         o[8] = vmax;
         o[9] = c;
     }

@@ -310,10 +310,12 @@ __device__ __forceinline__ void fold_stats(Table& T, const StageT& e, int s, Rec
             if (s == 0x7FFFFFF) atomicAdd(&C->pad[1], 1ull);
             return;
         }
-        atomicAdd(&T.sum[s], ds);
-        atomicAdd(&T.sq[s], dq);
-        atomicMin(&T.w[s][22], mn);
-        atomicMax(&T.w[s][23], mx);
+        if (!(ablate & 2048)) {
+            atomicAdd(&T.sum[s], ds);
+            atomicAdd(&T.sq[s], dq);
+            atomicMin(&T.w[s][22], mn);
+            atomicMax(&T.w[s][23], mx);
+        }
         const uint32_t old = atomicAdd(&T.w[s][21], n) & ~ADJ_FLAG;
         if (old + n > CNT_HARD) {
             // count bound: the samples' count and histogram go to a direct record
@@ -376,7 +378,15 @@ __device__ __forceinline__ void fold_batch(Table& T, const StageT* __restrict__ 
                 s = s < 0 ? s : (s & (INSERT_OVER - 1));
             }
         }
-        fold_stats<MODE, FAST40, StageT>(T, e[i], s, R, C, scale, offset, need, ablate);
+        int ab = ablate;
+        if (ablate & (512 | 1024)) {   // diagnostic: statistics atomics only at run heads
+            const uint32_t pu = (uint32_t)__builtin_amdgcn_update_dpp((int)e[i].x, (int)e[i].x, 0x138, 0xf, 0xf, false);
+            const uint32_t pv = (uint32_t)__builtin_amdgcn_update_dpp((int)e[i].y, (int)e[i].y, 0x138, 0xf, 0xf, false);
+            const bool hd = lane == 0 || pu != e[i].x || pv != e[i].y;
+            if (!hd) ab |= (ablate & 512) ? 2048 : 0;
+            if (!hd && (ablate & 1024)) ab |= 128;
+        }
+        fold_stats<MODE, FAST40, StageT>(T, e[i], s, R, C, scale, offset, need, ab);
     }
 }
 
@@ -422,10 +432,29 @@ __global__ __launch_bounds__(SCAN_THREADS, 4) void k_face_scan(ScanParams P, Rec
 
     const int Z = (int)P.shape[0], Y = (int)P.shape[1], X = (int)P.shape[2];
     const int64_t sz = (int64_t)Y * X;
-    const int x0 = (int)blockIdx.x * TILE_X;
+    // XCD-aware tile order: the hardware deals workgroups round-robin over the
+    // 8 XCDs (block b and b+8 share one), so block b takes tile t(b) with each
+    // XCD owning one contiguous run of tiles (x fastest, then y, then z).  The
+    // workgroups an XCD runs at a time are then x / y neighbours, and the
+    // x-halo column and y-halo row one tile reads are the rows its neighbour
+    // streams through the same L2, not a second HBM read.
+    int tx, ty, tz;
+    {
+        const uint32_t nwg = gridDim.x, id = blockIdx.x;
+        uint32_t t = id;
+        if (P.xcd_remap) {
+            const uint32_t q = nwg / 8, rm = nwg % 8, xcd = id % 8, j = id / 8;
+            t = xcd < rm ? xcd * (q + 1) + j : rm * (q + 1) + (xcd - rm) * q + j;
+        }
+        const uint32_t ntx = (uint32_t)P.ntiles[0], nty = (uint32_t)P.ntiles[1];
+        tx = (int)(t % ntx);
+        ty = (int)((t / ntx) % nty);
+        tz = (int)(t / (ntx * nty));
+    }
+    const int x0 = tx * TILE_X;
     const int x = x0 + lane;
-    const int yw = (int)blockIdx.y * WG_ROWS + wave * ROWS;   // first row of this wave (uniform)
-    const int z0 = (int)blockIdx.z * P.tile_z;
+    const int yw = ty * WG_ROWS + wave * ROWS;   // first row of this wave (uniform)
+    const int z0 = tz * P.tile_z;
     const int z1 = min(z0 + P.tile_z, Z);
     const LabelT* L = (const LabelT*)P.labels;
     const DataT* D = (const DataT*)P.data;
@@ -632,12 +661,18 @@ __global__ __launch_bounds__(SCAN_THREADS, 4) void k_face_scan(ScanParams P, Rec
 // ---------------------------------------------------------------------------
 template <typename LabelT, typename DataT, int MODE>
 static hipError_t launch_scan_t(const ScanParams& P, const RecordBuf& R, Counters* C, hipStream_t s) {
-    dim3 grid((unsigned)((P.shape[2] + TILE_X - 1) / TILE_X), (unsigned)((P.shape[1] + WG_ROWS - 1) / WG_ROWS),
-              (unsigned)((P.shape[0] + P.tile_z - 1) / P.tile_z));
+    ScanParams Q = P;
+    Q.ntiles[0] = (P.shape[2] + TILE_X - 1) / TILE_X;
+    Q.ntiles[1] = (P.shape[1] + WG_ROWS - 1) / WG_ROWS;
+    Q.ntiles[2] = (P.shape[0] + P.tile_z - 1) / P.tile_z;
+    const int64_t nwg = Q.ntiles[0] * Q.ntiles[1] * Q.ntiles[2];
+    if (nwg <= 0) return hipSuccess;
+    if (nwg > 0x7FFFFFFF) return hipErrorInvalidValue;
+    dim3 grid((unsigned)nwg);
     if (P.fast40)
-        hipLaunchKernelGGL((k_face_scan<LabelT, DataT, MODE, true>), grid, dim3(SCAN_THREADS), 0, s, P, R, C);
+        hipLaunchKernelGGL((k_face_scan<LabelT, DataT, MODE, true>), grid, dim3(SCAN_THREADS), 0, s, Q, R, C);
     else
-        hipLaunchKernelGGL((k_face_scan<LabelT, DataT, MODE, false>), grid, dim3(SCAN_THREADS), 0, s, P, R, C);
+        hipLaunchKernelGGL((k_face_scan<LabelT, DataT, MODE, false>), grid, dim3(SCAN_THREADS), 0, s, Q, R, C);
     return hipGetLastError();
 }
 
