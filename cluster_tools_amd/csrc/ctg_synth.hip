@@ -3,6 +3,8 @@
 // generator (integer geometry, correctly rounded double division, no FMA:
 // the library is built with -ffp-contract=off).  Used by bench.py to build the
 // BASELINE.json synthetic volumes directly in HBM.
+#include <algorithm>
+
 #include "ctg_internal.h"
 
 namespace ctg {
@@ -31,11 +33,8 @@ __device__ __forceinline__ int64_t seed_coord(const SynthParams& P, uint64_t cid
     return c * 256 * P.cell + (int64_t)(h % span);
 }
 
-__global__ __launch_bounds__(256) void k_synth(SynthParams P, uint64_t* __restrict__ labels,
-                                               float* __restrict__ boundary) {
-    const int64_t n = P.shape[0] * P.shape[1] * P.shape[2];
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
+__device__ __forceinline__ void synth_voxel(const SynthParams& P, int64_t i, uint64_t* __restrict__ labels,
+                                            float* __restrict__ boundary) {
     const int64_t X = P.shape[2], Y = P.shape[1];
     const int64_t x = i % X, y = (i / X) % Y, zl = i / (X * Y);
     const int64_t z = zl + P.z_offset;
@@ -80,16 +79,24 @@ __global__ __launch_bounds__(256) void k_synth(SynthParams P, uint64_t* __restri
     }
 }
 
+__global__ __launch_bounds__(256) void k_synth(SynthParams P, uint64_t* __restrict__ labels,
+                                               float* __restrict__ boundary) {
+    const int64_t n = P.shape[0] * P.shape[1] * P.shape[2];
+    // grid-stride: a launch covers at most 2^32 work-items (2048^3 volumes)
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        synth_voxel(P, i, labels, boundary);
+}
+
 __global__ void k_synth_aff(const float* __restrict__ b, float* __restrict__ out, int64_t Z, int64_t Y, int64_t X,
                             int oz, int oy, int ox) {
     const int64_t n = Z * Y * X;
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const int64_t x = i % X, y = (i / X) % Y, z = i / (X * Y);
-    const int64_t qz = z + oz, qy = y + oy, qx = x + ox;
-    float v = b[i];
-    if (qz >= 0 && qz < Z && qy >= 0 && qy < Y && qx >= 0 && qx < X) v = fmaxf(v, b[(qz * Y + qy) * X + qx]);
-    out[i] = v;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t x = i % X, y = (i / X) % Y, z = i / (X * Y);
+        const int64_t qz = z + oz, qy = y + oy, qx = x + ox;
+        float v = b[i];
+        if (qz >= 0 && qz < Z && qy >= 0 && qy < Y && qx >= 0 && qx < X) v = fmaxf(v, b[(qz * Y + qy) * X + qx]);
+        out[i] = v;
+    }
 }
 
 hipError_t launch_synth(uint64_t* labels, float* boundary, const int64_t* shape, int64_t z_offset,
@@ -108,7 +115,7 @@ hipError_t launch_synth(uint64_t* labels, float* boundary, const int64_t* shape,
     P.noise_amp = noise_amp;
     const int64_t n = shape[0] * shape[1] * shape[2];
     if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_synth, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, P, labels, boundary);
+    hipLaunchKernelGGL(k_synth, dim3((unsigned)std::min<int64_t>((n + 255) / 256, 1 << 20)), dim3(256), 0, s, P, labels, boundary);
     return hipGetLastError();
 }
 
@@ -117,7 +124,7 @@ hipError_t launch_synth_aff(const float* b, float* out, const int64_t* shape, in
     const int64_t n = shape[0] * shape[1] * shape[2];
     if (n == 0) return hipSuccess;
     for (int c = 0; c < n_channels; ++c) {
-        hipLaunchKernelGGL(k_synth_aff, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, b, out + (size_t)c * n,
+        hipLaunchKernelGGL(k_synth_aff, dim3((unsigned)std::min<int64_t>((n + 255) / 256, 1 << 20)), dim3(256), 0, s, b, out + (size_t)c * n,
                            shape[0], shape[1], shape[2], off[3 * c], off[3 * c + 1], off[3 * c + 2]);
     }
     return hipGetLastError();
