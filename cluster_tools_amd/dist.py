@@ -13,7 +13,11 @@ path is the merge: edges are range-partitioned by their lower label ``u``
 (splitters from an all-gathered sample, so the concatenation of the rank
 shards is the globally sorted edge table), the partial rows travel in one
 ``all_to_all_single`` (28 x int64 per edge: (u,v), (sum, sumsq), the 48-word
-wide record) and each rank merges what it received with ``ctg_merge_stats``.
+wide record).  Only rows that leave their rank are packed and shipped, and
+only keys present on more than one rank are merged (``ctg_merge_stats``):
+every other edge is complete in its slab and keeps the features of the local
+call.  With spatially ordered labels (the reference's block-offset watershed
+ids, the synthetic volumes) that is the few edges crossing a slab boundary.
 Node lists take the same route.  Scaling is weak: per-rank slab size is fixed.
 
 The exchange logic is backend-agnostic: ``HipBackend`` (libctg.so, the
@@ -43,14 +47,19 @@ class HipBackend:
                                     no_adj_filter=offsets is not None)
         keys = r.edges_torch_i64()
         sums, recs = r.stats_torch()
+        feats = r.features_torch()
         nodes = r.nodes_torch()
         info = r.info()
         r.free()
-        return keys, sums, recs, nodes, info
+        return keys, sums, recs, nodes, info, feats
 
     def merge(self, keys, sums, recs, hist_range):
+        """Merged (edges (E,2) int64, features (E,10) float64) tensors."""
         from . import rag
-        return rag.merge_stats_handle(keys, sums, recs, hist_range=hist_range)
+        m = rag.merge_stats_handle(keys, sums, recs, hist_range=hist_range)
+        out = m.edges_torch_i64(), m.features_torch()
+        m.free()
+        return out
 
     def unique(self, values):
         from . import rag
@@ -113,19 +122,48 @@ def split_counts(sorted_keys, splitters):
     return [bounds[i + 1] - bounds[i] for i in range(len(bounds) - 1)]
 
 
+def _wire_device(device, group):
+    """Where collectives run: RCCL ("nccl") moves HBM tensors over xGMI; a
+    gloo group (CPU tests, and the multi-process GPU test on a one-GPU box)
+    stages device tensors through host memory."""
+    return torch.device('cpu') if dist.get_backend(group) == 'gloo' else device
+
+
 def exchange(rows, send_counts, group=None):
     """all_to_all of variable-length row blocks; returns the received rows."""
     world = dist.get_world_size(group)
     dev = rows.device
-    sc = torch.tensor(send_counts, dtype=torch.int64, device=dev)
-    rc = torch.empty(world, dtype=torch.int64, device=dev)
+    wire = _wire_device(dev, group)
+    sc = torch.tensor(send_counts, dtype=torch.int64, device=wire)
+    rc = torch.empty(world, dtype=torch.int64, device=wire)
     dist.all_to_all_single(rc, sc, group=group)
     recv_counts = rc.cpu().tolist()
     shape = (sum(recv_counts),) + tuple(rows.shape[1:])
-    out = torch.empty(shape, dtype=rows.dtype, device=dev)
-    dist.all_to_all_single(out, rows.contiguous(), output_split_sizes=recv_counts,
+    out = torch.empty(shape, dtype=rows.dtype, device=wire)
+    dist.all_to_all_single(out, rows.contiguous().to(wire), output_split_sizes=recv_counts,
                            input_split_sizes=list(send_counts), group=group)
-    return out
+    return out.to(dev)
+
+
+def all_gather_tensor(t, group=None):
+    """all_gather of equal-shape tensors -> list (on t's device)."""
+    wire = _wire_device(t.device, group)
+    tw = t.to(wire)
+    out = [torch.empty_like(tw) for _ in range(dist.get_world_size(group))]
+    dist.all_gather(out, tw, group=group)
+    return [x.to(t.device) for x in out]
+
+
+def _pack_uv(k):
+    """(E,2) int64 (u,v) -> one sortable int64 (labels < 2^31)."""
+    return k[:, 0] * (1 << 32) + k[:, 1]
+
+
+def _tensor(x, like):
+    if isinstance(x, torch.Tensor):
+        return x
+    return torch.as_tensor(np.asarray(x).astype(np.int64) if np.asarray(x).dtype == np.uint64 else np.asarray(x),
+                           device=like.device)
 
 
 class DistResult:
@@ -142,30 +180,32 @@ class DistResult:
 
     @property
     def n_edges(self):
-        m = self.merged
-        return m.n_edges if hasattr(m, 'n_edges') else int(m['edges'].shape[0])
+        return int(self.merged['edges'].shape[0])
 
     def info(self):
         return self._info
 
     def edges(self):
-        m = self.merged
-        return m.edges() if hasattr(m, 'edges') and callable(m.edges) else m['edges']
+        """(E,2) uint64 numpy array."""
+        e = self.merged['edges']
+        if isinstance(e, torch.Tensor):
+            e = e.cpu().numpy()
+        return np.asarray(e).astype(np.uint64)
 
     def features(self):
-        m = self.merged
-        return m.features() if hasattr(m, 'features') and callable(m.features) else m['features']
+        """(E,10) float64 numpy array."""
+        f = self.merged['features']
+        if isinstance(f, torch.Tensor):
+            f = f.cpu().numpy()
+        return np.asarray(f)
 
     def free(self):
-        if hasattr(self.merged, 'free'):
-            self.merged.free()
+        self.merged = {'edges': self.merged['edges'][:0], 'features': self.merged['features'][:0]}
 
 
 def _exclusive_offset(n_local, group, device):
-    world = dist.get_world_size(group)
     t = torch.tensor([n_local], dtype=torch.int64, device=device)
-    allc = [torch.empty_like(t) for _ in range(world)]
-    dist.all_gather(allc, t, group=group)
+    allc = all_gather_tensor(t, group)
     counts = [int(x.item()) for x in allc]
     r = dist.get_rank(group)
     return sum(counts[:r]), sum(counts)
@@ -182,29 +222,66 @@ def rag_features_distributed(labels, data=None, offsets=None, own_begin=None, ow
     """
     backend = backend or HipBackend()
     world = dist.get_world_size(group)
-    keys, sums, recs, nodes, info = backend.local(labels, data, offsets, own_begin, own_end,
-                                                  ignore_label, hist_range)
+    rank = dist.get_rank(group)
+    keys, sums, recs, nodes, info, feats = backend.local(labels, data, offsets, own_begin, own_end,
+                                                         ignore_label, hist_range)
     dev = keys.device
     n = keys.shape[0]
-    # splitters on u from an evenly spaced sample of the sorted local keys
+    # splitters on u from an evenly spaced sample of the sorted local keys; the
+    # largest label rides along (packed (u,v) keys need labels < 2^31)
     if n > 0:
         idx = torch.div(torch.arange(N_SAMPLES, device=dev, dtype=torch.int64) * n, N_SAMPLES,
                         rounding_mode='floor')
         samp = keys[:, 0].index_select(0, idx)
+        vmax = keys[:, 1].max().reshape(1)
     else:
         samp = torch.zeros(N_SAMPLES, dtype=torch.int64, device=dev)
-    meta = torch.cat([samp, torch.tensor([n], dtype=torch.int64, device=dev)])
-    gathered = [torch.empty_like(meta) for _ in range(world)]
-    dist.all_gather(gathered, meta, group=group)
-    g = torch.stack(gathered).cpu().numpy()
+        vmax = torch.zeros(1, dtype=torch.int64, device=dev)
+    meta = torch.cat([samp, torch.tensor([n], dtype=torch.int64, device=dev), vmax])
+    g = torch.stack(all_gather_tensor(meta, group)).cpu().numpy()
     splitters = weighted_splitters(g[:, :N_SAMPLES], g[:, N_SAMPLES], world)
+    counts = split_counts(keys[:, 0], splitters)
+    packable = int(g[:, N_SAMPLES + 1].max()) < (1 << 31) and int(nodes.max().item() if nodes.numel() else 0) < (1 << 31)
 
-    # edge rows -> owner of u
-    rows = pack_rows(keys, sums, recs)
-    recv = exchange(rows, split_counts(keys[:, 0], splitters), group)
-    rk, rs, rr = unpack_rows(recv)
-    merged = backend.merge(rk, rs, rr, hist_range)
-    n_loc = merged.n_edges if hasattr(merged, 'n_edges') else int(merged['edges'].shape[0])
+    if not packable:
+        # general labels: every row goes to the owner of its u and is merged there
+        rows = pack_rows(keys, sums, recs)
+        recv = exchange(rows, counts, group)
+        rk, rs, rr = unpack_rows(recv)
+        me, mf = backend.merge(rk, rs, rr, hist_range)
+        merged = {'edges': me, 'features': mf}
+    else:
+        # rows of other owners leave; this rank's own block stays in place
+        lo = sum(counts[:rank])
+        hi = lo + counts[rank]
+        send = list(counts)
+        send[rank] = 0
+        out_k = torch.cat([keys[:lo], keys[hi:]])
+        out_rows = pack_rows(out_k, torch.cat([sums[:lo], sums[hi:]]), torch.cat([recs[:lo], recs[hi:]]))
+        recv = exchange(out_rows, send, group)
+        lk, ls, lr, lf = keys[lo:hi], sums[lo:hi], recs[lo:hi], feats[lo:hi]
+        if recv.shape[0] == 0:
+            shared = torch.zeros(lk.shape[0], dtype=torch.bool, device=dev)
+        else:
+            rk, rs, rr = unpack_rows(recv)
+            shared = torch.isin(_pack_uv(lk), _pack_uv(rk))
+        # local-only keys are final; with affinities a key must have been seen
+        # on a nearest-neighbour face (ADJ bit of its wide record)
+        keep = ~shared
+        if offsets is not None:
+            keep &= lr[:, 42] < 0
+        if recv.shape[0] == 0:
+            merged = {'edges': lk[keep], 'features': lf[keep]}
+        else:
+            me, mf = backend.merge(torch.cat([rk, lk[shared]]), torch.cat([rs, ls[shared]]),
+                                   torch.cat([rr, lr[shared]]), hist_range)
+            me = _tensor(me, lk)
+            mf = _tensor(mf, lf)
+            ak = torch.cat([lk[keep], me])
+            af = torch.cat([lf[keep], mf])
+            order = torch.argsort(_pack_uv(ak))
+            merged = {'edges': ak[order], 'features': af[order]}
+    n_loc = int(merged['edges'].shape[0])
 
     # nodes -> the same ranges
     nrecv = exchange(nodes.reshape(-1), split_counts(nodes.reshape(-1), splitters), group)

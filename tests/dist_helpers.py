@@ -56,22 +56,24 @@ def decode_stats(sums, rec):
 class OracleBackend:
     def local(self, labels, data, offsets, own_begin, own_end, ignore_label, hist_range):
         lab = np.asarray(labels)
-        edges, _, stats = O.boundary_features(lab, np.asarray(data), own_begin=own_begin,
-                                              ignore_label=ignore_label, lo=hist_range[0], hi=hist_range[1],
-                                              return_stats=True)
+        edges, feats, stats = O.boundary_features(lab, np.asarray(data), own_begin=own_begin,
+                                                  ignore_label=ignore_label, lo=hist_range[0], hi=hist_range[1],
+                                                  return_stats=True)
         sums, rec = encode_stats(stats)
         nodes = np.unique(edges.reshape(-1))
         return (torch.from_numpy(edges.astype(np.int64)), torch.from_numpy(sums),
-                torch.from_numpy(rec.view(np.int32)), torch.from_numpy(nodes.astype(np.int64)), (0, 0))
+                torch.from_numpy(rec.view(np.int32)), torch.from_numpy(nodes.astype(np.int64)), (0, 0),
+                torch.from_numpy(np.ascontiguousarray(feats)))
 
     def merge(self, keys, sums, recs, hist_range):
         k = keys.numpy().astype(np.uint64)
         if k.shape[0] == 0:
-            return dict(edges=np.zeros((0, 2), np.uint64), features=np.zeros((0, O.N_FEATURES)))
+            return torch.zeros((0, 2), dtype=torch.int64), torch.zeros((0, O.N_FEATURES), dtype=torch.float64)
         edges, inv = O._unique_pairs(k, return_inverse=True)
         st = decode_stats(sums.numpy(), recs.numpy().view(np.uint32))
         merged = O.merge_feature_stats([(inv, st)], edges.shape[0], hist_range[0], hist_range[1])
-        return dict(edges=edges, features=O.finalize_features(merged, hist_range[0], hist_range[1]))
+        feats = O.finalize_features(merged, hist_range[0], hist_range[1])
+        return torch.from_numpy(edges.astype(np.int64)), torch.from_numpy(np.ascontiguousarray(feats))
 
     def unique(self, values):
         return torch.from_numpy(np.unique(values.numpy()))

@@ -27,13 +27,23 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, shape, cell, outdir, ignore_label):
+BIG = 1 << 33   # labels >= 2^31: the exchange falls back to merging every row
+
+
+def _volume(shape, cell, big):
+    lab, bnd = synthetic.generate(shape, cell=cell, seed=3)
+    if big:
+        lab = lab + np.uint64(BIG)
+    return lab, bnd
+
+
+def _worker(rank, world, port, shape, cell, outdir, ignore_label, big=False):
     import torch.distributed as dist
     from tests.dist_helpers import OracleBackend
     os.environ['MASTER_ADDR'] = '127.0.0.1'
     os.environ['MASTER_PORT'] = str(port)
     dist.init_process_group('gloo', rank=rank, world_size=world)
-    lab, bnd = synthetic.generate(shape, cell=cell, seed=3)
+    lab, bnd = _volume(shape, cell, big)
     Z = shape[0]
     z0 = [Z * r // world for r in range(world + 1)]
     halo = 1 if rank > 0 else 0
@@ -49,13 +59,14 @@ def _worker(rank, world, port, shape, cell, outdir, ignore_label):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize('world,shape,cell,ignore', [
-    (2, (24, 40, 36), 6, False),
-    (3, (30, 33, 29), 5, True),
+@pytest.mark.parametrize('world,shape,cell,ignore,big', [
+    (2, (24, 40, 36), 6, False, False),
+    (3, (30, 33, 29), 5, True, False),
+    (2, (20, 30, 28), 5, False, True),
 ])
-def test_distributed_matches_whole_volume(tmp_path, world, shape, cell, ignore):
-    mp.spawn(_worker, args=(world, _free_port(), shape, cell, str(tmp_path), ignore), nprocs=world, join=True)
-    lab, bnd = synthetic.generate(shape, cell=cell, seed=3)
+def test_distributed_matches_whole_volume(tmp_path, world, shape, cell, ignore, big):
+    mp.spawn(_worker, args=(world, _free_port(), shape, cell, str(tmp_path), ignore, big), nprocs=world, join=True)
+    lab, bnd = _volume(shape, cell, big)
     e_ref, f_ref = O.boundary_features(lab, bnd, ignore_label=ignore)
     nodes_ref = O.unique_labels(O.rag_edges(lab))  # endpoints of the unfiltered RAG
     es = [np.load(tmp_path / ('e%d.npy' % r)) for r in range(world)]
