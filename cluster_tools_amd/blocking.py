@@ -55,6 +55,15 @@ class blocking:  # noqa: N801  (nifty's spelling)
     def gridPositionToBlockId(self, pos):  # noqa: N802
         return int(sum(p * s for p, s in zip(pos, self._strides)))
 
+    def getNeighborId(self, block_id, axis, lower):  # noqa: N802
+        """Id of the neighbouring block along ``axis`` (the lower one if
+        ``lower``), -1 past the grid (mutex_watershed/two_pass_mws.py:241)."""
+        pos = self.blockGridPosition(block_id)
+        pos[axis] += -1 if lower else 1
+        if not 0 <= pos[axis] < self.blocksPerAxis[axis]:
+            return -1
+        return self.gridPositionToBlockId(pos)
+
     def getBlock(self, block_id):  # noqa: N802
         if not 0 <= block_id < self.numberOfBlocks:
             raise IndexError('block id %d out of range' % block_id)

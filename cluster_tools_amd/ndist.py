@@ -229,6 +229,58 @@ class Graph:
     def findEdge(self, u, v):  # noqa: N802
         return int(self.findEdges(np.array([[u, v]], dtype=np.uint64))[0])
 
+    def extractSubgraphFromNodes(self, nodes, allowInvalidNodes=False):  # noqa: N802,N803
+        """(inner_edges, outer_edges): ids of the edges with both / exactly one
+        endpoint in ``nodes`` (multicut/solve_subproblems.py:154,
+        lifted_multicut/solve_lifted_subproblems.py:170), ascending.  Without
+        allowInvalidNodes a node id that is not in the graph raises, as nifty
+        does."""
+        nodes = np.asarray(nodes, dtype=np.uint64).reshape(-1)
+        if not allowInvalidNodes and nodes.size:
+            known = np.isin(nodes, self._nodes)
+            if not known.all():
+                raise RuntimeError('extractSubgraphFromNodes: node %d is not in the graph'
+                                   % int(nodes[~known][0]))
+        in_u = np.isin(self._uv[:, 0], nodes)
+        in_v = np.isin(self._uv[:, 1], nodes)
+        inner = np.flatnonzero(in_u & in_v).astype(np.int64)
+        outer = np.flatnonzero(in_u ^ in_v).astype(np.int64)
+        return inner, outer
+
+    def flattenedNeighborhoods(self):  # noqa: N802
+        """The node part of vigra's AdjacencyListGraph serialisation, as
+        ilastik/carving.py:43 consumes it: for every node in ascending id
+        order its degree, then (neighbour id, edge id) per neighbour in
+        ascending neighbour order.  (Format restated from vigra's
+        adjacency_list_graph.hxx serialize; no reference fixture pins it.)"""
+        uv = self._uv
+        E = uv.shape[0]
+        eid = np.arange(E, dtype=np.uint64)
+        # both directions of every edge, sorted by (node, neighbour)
+        a = np.concatenate([uv[:, 0], uv[:, 1]])
+        b = np.concatenate([uv[:, 1], uv[:, 0]])
+        e = np.concatenate([eid, eid])
+        order = np.lexsort((b, a))
+        a, b, e = a[order], b[order], e[order]
+        nodes = self._nodes
+        deg = np.zeros(nodes.shape[0], dtype=np.uint64)
+        if E:
+            idx = np.searchsorted(nodes, a)
+            np.add.at(deg, idx, 1)
+        out = np.empty(nodes.shape[0] + 2 * a.shape[0], dtype=np.uint64)
+        # layout: for node k at offset off[k]: deg, then 2*deg entries
+        off = np.zeros(nodes.shape[0], dtype=np.int64)
+        if nodes.shape[0] > 1:
+            off[1:] = np.cumsum(1 + 2 * deg[:-1].astype(np.int64))
+        out[off] = deg
+        if E:
+            start = np.repeat(off + 1, deg.astype(np.int64))
+            rank = np.arange(a.shape[0]) - np.repeat(np.cumsum(deg.astype(np.int64)) - deg.astype(np.int64),
+                                                     deg.astype(np.int64))
+            out[start + 2 * rank] = b
+            out[start + 2 * rank + 1] = e
+        return out
+
 
 # ---------------------------------------------------------------------------
 # features

@@ -124,3 +124,37 @@ def test_synthetic_edge_density():
     n_nodes = O.unique_labels(lab).size
     n_edges = O.rag_edges(lab).shape[0]
     assert 40 <= n_nodes <= 130 and 4 * n_nodes <= n_edges <= 12 * n_nodes
+
+
+def test_graph_subgraph_and_neighborhoods():
+    """ndist.Graph.extractSubgraphFromNodes / flattenedNeighborhoods against
+    a direct restatement over python sets."""
+    from cluster_tools_amd import ndist
+    uv = np.array([[1, 2], [1, 5], [2, 3], [3, 5], [5, 9]], dtype=np.uint64)
+    g = ndist.Graph(uv)
+    inner, outer = g.extractSubgraphFromNodes([1, 2, 3])
+    np.testing.assert_array_equal(inner, [0, 2])
+    np.testing.assert_array_equal(outer, [1, 3])
+    with pytest.raises(RuntimeError):
+        g.extractSubgraphFromNodes([1, 4])
+    inner, outer = g.extractSubgraphFromNodes([1, 4], allowInvalidNodes=True)
+    assert inner.size == 0 and list(outer) == [0, 1]
+    flat = g.flattenedNeighborhoods()
+    ref = []
+    for n in [1, 2, 3, 5, 9]:
+        nb = sorted((int(b if a == n else a), e) for e, (a, b) in enumerate(uv.tolist()) if n in (a, b))
+        ref.append(len(nb))
+        for other, e in nb:
+            ref += [other, e]
+    np.testing.assert_array_equal(flat, np.array(ref, dtype=np.uint64))
+
+
+def test_blocking_neighbor_ids():
+    from cluster_tools_amd.blocking import blocking
+    b = blocking([0, 0, 0], [10, 20, 30], [5, 10, 10])   # 2 x 2 x 3 blocks
+    assert b.numberOfBlocks == 12
+    bid = b.gridPositionToBlockId([1, 0, 1])
+    assert b.getNeighborId(bid, 0, True) == b.gridPositionToBlockId([0, 0, 1])
+    assert b.getNeighborId(bid, 0, False) == -1
+    assert b.getNeighborId(bid, 1, True) == -1
+    assert b.getNeighborId(bid, 2, False) == b.gridPositionToBlockId([1, 0, 2])
