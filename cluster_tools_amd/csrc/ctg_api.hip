@@ -668,6 +668,9 @@ int ctg_rag_features(const void* labels, int label_bits, const void* data, int d
         }
     }
     const int64_t n = (int64_t)w.counters_host->n_records;
+    if (P.ablate & 256)   // diagnostic s_memtime stamps, summed over waves
+        fprintf(stderr, "stamps total %llu fold %llu flush %llu wait %llu\n", w.counters_host->pad[2],
+                w.counters_host->pad[3], w.counters_host->pad[4], w.counters_host->pad[5]);
     w.last_records = n;
     w.last_direct = (int64_t)w.counters_host->n_direct;
 

@@ -103,7 +103,7 @@ struct Counters {               // device-side counters, zeroed per call
     unsigned long long n_direct;     // faces emitted past a full LDS table
     unsigned long long label_overflow;  // labels >= 2^32 seen by the 32-bit key path
     unsigned long long max_v;        // largest label in any key
-    unsigned long long pad[4];
+    unsigned long long pad[8];      // diagnostics (ablation checks, s_memtime stamps)
 };
 
 struct ReduceOut {

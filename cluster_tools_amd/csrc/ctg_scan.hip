@@ -402,6 +402,13 @@ __device__ __forceinline__ bool adj_contains(const unsigned long long* __restric
     }
 }
 
+// diagnostic time stamp (volatile: never merged or moved across other code)
+__device__ __forceinline__ uint64_t stamp_now() {
+    uint64_t t;
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    return t;
+}
+
 // x-neighbour of every lane: lane i gets lane i+1 (DPP wave_shl:1), lane 63
 // gets `edge` (the x-halo value)
 __device__ __forceinline__ uint32_t shl1(uint32_t v, uint32_t edge) {
@@ -524,6 +531,10 @@ __global__ __launch_bounds__(SCAN_THREADS, 4) void k_face_scan(ScanParams P, Rec
     // so a request never waits for a wave that has left the loop.
     bool need = false;
     int nbuf = 0;   // staged entries (wave-uniform)
+    // diagnostic 256: s_memtime stamps per wave (fold, flush, prefetch wait, total)
+    const bool stamps = (ablate & 256) != 0;
+    uint64_t t_fold = 0, t_flush = 0, t_wait = 0;
+    const uint64_t t_start = stamps ? stamp_now() : 0;
     auto poll = [&]() {
         if (__ballot(need)) {
             if (lane == 0) atomicOr(&T.flush_req, 1u);
@@ -531,12 +542,18 @@ __global__ __launch_bounds__(SCAN_THREADS, 4) void k_face_scan(ScanParams P, Rec
         }
         const uint32_t fr = (uint32_t)__builtin_amdgcn_readfirstlane(
             (int)__hip_atomic_load(&T.flush_req, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
-        if (fr) table_flush<MODE>(T, R, C);
+        if (fr) {
+            const uint64_t t0 = stamps ? stamp_now() : 0;
+            table_flush<MODE>(T, R, C);
+            if (stamps) t_flush += stamp_now() - t0;
+        }
     };
     auto flush_stage = [&]() {
         if (nbuf) {
+            const uint64_t t0 = stamps ? stamp_now() : 0;
             fold_batch<MODE, FAST40, StageT, NPER>(T, stage, nbuf, lane, R, C, scale, offset, need, ablate);
             nbuf = 0;
+            if (stamps) t_fold += stamp_now() - t0;
             poll();
         }
     };
@@ -616,6 +633,11 @@ __global__ __launch_bounds__(SCAN_THREADS, 4) void k_face_scan(ScanParams P, Rec
                 }
             }
             // z faces: plane z against the prefetched plane z+1
+            if (stamps) {
+                const uint64_t t0 = stamp_now();
+                __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): the prefetched plane has landed
+                t_wait += stamp_now() - t0;
+            }
             if (zup) {
 #pragma unroll
                 for (int r = 0; r < ROWS; ++r) {
@@ -654,6 +676,12 @@ __global__ __launch_bounds__(SCAN_THREADS, 4) void k_face_scan(ScanParams P, Rec
         __builtin_amdgcn_s_sleep(2);
     }
     table_flush<MODE>(T, R, C);
+    if (stamps && lane == 0) {
+        atomicAdd(&C->pad[2], (unsigned long long)(stamp_now() - t_start));
+        atomicAdd(&C->pad[3], (unsigned long long)t_fold);
+        atomicAdd(&C->pad[4], (unsigned long long)t_flush);
+        atomicAdd(&C->pad[5], (unsigned long long)t_wait);
+    }
 }
 
 // ---------------------------------------------------------------------------
