@@ -557,7 +557,7 @@ int ctg_rag_features(const void* labels, int label_bits, const void* data, int d
     P.offset = hist_lo;
     P.fast40 = (hist_lo == 0.0 && P.scale == 40.0) ? 1 : 0;
     // flush decisions every check_planes planes (overflow safety does not
-    // depend on it: ctg_scan.hip bounds each entry's count in the fold)
+    // depend on it: ctg_scan.hip's per-wave sample budget bounds every count)
     P.check_planes = 8;
     if (const char* cp = getenv("CTG_CHECK_PLANES")) P.check_planes = std::max(1, atoi(cp));
     // planes per workgroup: deep tiles (fewer records), but >= ~1024 workgroups

@@ -23,15 +23,14 @@
 // sum of squares, order-preserving min / max and the 42-slot vigra histogram
 // (u16 slots in u32 words).
 //
-// Overflow safety without barriers.  The count word is added with a returning
-// atomic before the histogram add: a slot can never exceed the entry's count,
-// so as long as every accepted add keeps the count <= 65535 no u16 slot can
-// wrap.  A face that would push the count past 65535 goes to HBM as a direct
-// record instead (its sum / min / max are already in the table entry: records
-// of one key are additive, so splitting a face's contributions between two
-// records is exact).  Table fill and count pressure only set a per-lane
-// "need flush" flag; the wave then raises the workgroup's flush request, which
-// every wave polls after each fold batch and plane (see k_face_scan).
+// Overflow safety without returning atomics.  A histogram slot never exceeds
+// its entry's count, and an entry's count never exceeds the samples the eight
+// waves folded since the last table flush.  Each wave keeps a sample budget of
+// 65535 / 8 per flush interval: before a fold batch that would pass it, the
+// wave forces a flush.  So no u16 slot can wrap, and every statistics update
+// is a fire-and-forget LDS atomic.  Table fill only sets a per-lane "need
+// flush" flag; the wave then raises the workgroup's flush request, which every
+// wave polls after each fold batch and plane (see k_face_scan).
 #include <type_traits>
 
 #include "ctg_internal.h"
@@ -52,8 +51,10 @@ constexpr int WG_ROWS = ROWS * WAVES;                     // tile y extent
 #endif
 constexpr int NPER = CTG_NPER;                            // staged entries folded per lane
 constexpr int STAGE_CAP = WAVE * NPER;                    // stage entries per wave
-constexpr uint32_t CNT_HARD = 65535u;                     // u16 histogram slots: count bound
-constexpr uint32_t CNT_SOFT = 40000u;                     // ask for a flush past this count
+// u16 histogram slots: a table entry holds at most 65535 samples.  Each wave
+// folds at most this many samples between two table flushes (it requests a
+// flush before a batch would exceed it), so no entry can pass the bound.
+constexpr uint32_t WAVE_SAMPLE_BUDGET = 65535u / WAVES;
 #ifndef CTG_FILL_SOFT
 #define CTG_FILL_SOFT (TABLE_CAP / 2)
 #endif
@@ -173,8 +174,7 @@ __device__ __noinline__ void table_flush(Table& T, RecordBuf R, Counters* C) {
     lds_barrier();
 }
 
-// One record straight to HBM: a key that found no room in the table, or the
-// count / histogram part of samples whose table entry is at its count bound.
+// One record straight to HBM: a key that found no room in the table.
 // sa / sb: histogram slots of the samples (-1: none); s / q / mn / mx: the
 // sum, sum of squares and ordered min / max this record carries.
 __device__ __noinline__ void emit_direct(RecordBuf R, Counters* C, uint64_t key, uint32_t cnt_flag, int sa, int sb,
@@ -310,21 +310,13 @@ __device__ __forceinline__ void fold_stats(Table& T, const StageT& e, int s, Rec
             if (s == 0x7FFFFFF) atomicAdd(&C->pad[1], 1ull);
             return;
         }
-        if (!(ablate & 2048)) {
-            atomicAdd(&T.sum[s], ds);
-            atomicAdd(&T.sq[s], dq);
-            atomicMin(&T.w[s][22], mn);
-            atomicMax(&T.w[s][23], mx);
-        }
-        const uint32_t old = atomicAdd(&T.w[s][21], n) & ~ADJ_FLAG;
-        if (old + n > CNT_HARD) {
-            // count bound: the samples' count and histogram go to a direct record
-            atomicSub(&T.w[s][21], n);
-            need = true;
-            emit_direct(R, C, key, n, sa, sb, 0.0, 0.0, ORD_POS_INF, ORD_NEG_INF, true);
-            return;
-        }
-        if (old + n > CNT_SOFT) need = true;
+        // fire-and-forget adds: the per-wave sample budget (k_face_scan) keeps
+        // every count, hence every u16 histogram slot, below 2^16
+        atomicAdd(&T.sum[s], ds);
+        atomicAdd(&T.sq[s], dq);
+        atomicMin(&T.w[s][22], mn);
+        atomicMax(&T.w[s][23], mx);
+        atomicAdd(&T.w[s][21], n);
         if (ablate & 128) return;   // diagnostic: no histogram
         if constexpr (BND) hist_add2(T, s, sa, sb);
         else atomicAdd(&T.w[s][sa >> 1], 1u << ((sa & 1) * 16));
@@ -378,15 +370,7 @@ __device__ __forceinline__ void fold_batch(Table& T, const StageT* __restrict__ 
                 s = s < 0 ? s : (s & (INSERT_OVER - 1));
             }
         }
-        int ab = ablate;
-        if (ablate & (512 | 1024)) {   // diagnostic: statistics atomics only at run heads
-            const uint32_t pu = (uint32_t)__builtin_amdgcn_update_dpp((int)e[i].x, (int)e[i].x, 0x138, 0xf, 0xf, false);
-            const uint32_t pv = (uint32_t)__builtin_amdgcn_update_dpp((int)e[i].y, (int)e[i].y, 0x138, 0xf, 0xf, false);
-            const bool hd = lane == 0 || pu != e[i].x || pv != e[i].y;
-            if (!hd) ab |= (ablate & 512) ? 2048 : 0;
-            if (!hd && (ablate & 1024)) ab |= 128;
-        }
-        fold_stats<MODE, FAST40, StageT>(T, e[i], s, R, C, scale, offset, need, ab);
+        fold_stats<MODE, FAST40, StageT>(T, e[i], s, R, C, scale, offset, need, ablate);
     }
 }
 
@@ -530,7 +514,8 @@ __global__ __launch_bounds__(SCAN_THREADS, 4) void k_face_scan(ScanParams P, Rec
     // Waves done with their planes keep polling until the last one is done,
     // so a request never waits for a wave that has left the loop.
     bool need = false;
-    int nbuf = 0;   // staged entries (wave-uniform)
+    int nbuf = 0;         // staged entries (wave-uniform)
+    uint32_t wsamp = 0;   // samples this wave folded since the last flush (wave-uniform)
     // diagnostic 256: s_memtime stamps per wave (fold, flush, prefetch wait, total)
     const bool stamps = (ablate & 256) != 0;
     uint64_t t_fold = 0, t_flush = 0, t_wait = 0;
@@ -545,11 +530,21 @@ __global__ __launch_bounds__(SCAN_THREADS, 4) void k_face_scan(ScanParams P, Rec
         if (fr) {
             const uint64_t t0 = stamps ? stamp_now() : 0;
             table_flush<MODE>(T, R, C);
+            wsamp = 0;
             if (stamps) t_flush += stamp_now() - t0;
         }
     };
     auto flush_stage = [&]() {
         if (nbuf) {
+            if constexpr (STATS) {
+                // per-wave sample budget: flush first if this batch would pass it
+                const uint32_t add = BND ? 2u * (uint32_t)nbuf : (uint32_t)nbuf;
+                if (wsamp + add > WAVE_SAMPLE_BUDGET) {
+                    need = true;
+                    poll();
+                }
+                wsamp += add;
+            }
             const uint64_t t0 = stamps ? stamp_now() : 0;
             fold_batch<MODE, FAST40, StageT, NPER>(T, stage, nbuf, lane, R, C, scale, offset, need, ablate);
             nbuf = 0;

@@ -201,6 +201,29 @@ def test_many_edges_per_tile(gpu):
     check_features(out['features'], f_ref)
 
 
+def test_single_edge_past_u16_count(gpu, monkeypatch):
+    """Labels alternate in x, so every x face of a 64x32x64 tile is the same edge
+    (1,2): ~260 K samples per tile, all in two histogram slots.  Without the
+    per-wave sample budget of the scan those u16 slots would wrap and q25 / q75
+    would land 16 bins off."""
+    monkeypatch.setenv('CTG_TILE_Z', '64')
+    shape = (64, 64, 128)
+    x = np.arange(shape[2])
+    lab = np.broadcast_to((x % 2 + 1).astype(np.uint64), shape).copy()
+    bnd = np.broadcast_to(np.where(x % 2, 0.7, 0.3).astype(np.float32), shape).copy()
+    e_ref, f_ref = O.boundary_features(lab, bnd)
+    out = rag.rag_features(lab, bnd)
+    np.testing.assert_array_equal(out['edges'], e_ref)
+    check_features(out['features'], f_ref)
+    assert out['features'][0, 9] > 4 * 65535
+    offsets = S.NN_OFFSETS
+    affs = np.stack([np.full(shape, 0.2 + 0.3 * c, np.float32) for c in range(len(offsets))])
+    e_ref, f_ref = O.affinity_features(lab, affs, offsets)
+    out = rag.rag_features(lab, affs, offsets=offsets)
+    np.testing.assert_array_equal(out['edges'], e_ref)
+    check_features(out['features'], f_ref)
+
+
 def test_salt_and_pepper_labels(gpu):
     """Random labels: almost every face is a boundary face with a new key."""
     rng = np.random.default_rng(1)
