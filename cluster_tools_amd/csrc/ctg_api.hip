@@ -21,6 +21,8 @@ int scan_tile_rows();
 hipError_t launch_unique_tiles(const uint64_t* L, const int64_t* shape, const int64_t* b, const int64_t* e,
                                uint64_t* out, unsigned long long* count, int64_t cap, hipStream_t s);
 hipError_t launch_pack_keys(int64_t n, const uint64_t* key, int nb, uint64_t* sk, uint32_t* idx, hipStream_t s);
+hipError_t launch_pack_regions(const uint64_t* key, int64_t rcap, const RegionPrefix& pre, int nb, uint64_t* sk,
+                               uint32_t* idx, hipStream_t s);
 hipError_t launch_pack_pairs(int64_t n, const uint64_t* uv, int nb, uint64_t* sk, uint32_t* idx, hipStream_t s);
 hipError_t launch_max_pairs(int64_t n, const uint64_t* uv, unsigned long long* out, hipStream_t s);
 hipError_t launch_reduce(int64_t E, const uint32_t* dE, const uint64_t* uniq, const uint32_t* runs,
@@ -155,6 +157,7 @@ hipError_t ensure_records(Workspace& w, int64_t need, int wide) {
     w.rec.hist = (uint32_t*)dalloc((size_t)need * words * 4);
     if (!w.rec.key || (wide && !w.rec.sums) || !w.rec.hist) return hipErrorOutOfMemory;
     w.rec.cap = need;
+    w.rec.rcap = need / NREG;
     return hipSuccess;
 }
 
@@ -201,6 +204,7 @@ struct ReduceJob {
     double scale, offset;
     int64_t single_label_nodes;  // >=0: no edges -> nodes = this label; -1: none
     const uint64_t* single_label_ptr;  // device pointer to a label to use if E == 0
+    const RegionPrefix* regions;       // keys in NREG regions of R (scan records), or null: dense
 };
 
 static hipError_t reduce_records(Workspace& w, const ReduceJob& J, hipStream_t s, ctg_result* res) {
@@ -249,7 +253,8 @@ static hipError_t reduce_records(Workspace& w, const ReduceJob& J, hipStream_t s
     uint32_t* dE = w.small + 1;
     uint32_t* dN = w.small + 2;
     hipError_t e;
-    if (J.keys) e = launch_pack_keys(n, J.keys, nb, w.sk_in, w.idx_in, s);
+    if (J.keys && J.regions) e = launch_pack_regions(J.keys, J.R.rcap, *J.regions, nb, w.sk_in, w.idx_in, s);
+    else if (J.keys) e = launch_pack_keys(n, J.keys, nb, w.sk_in, w.idx_in, s);
     else e = launch_pack_pairs(n, J.pairs, nb, w.sk_in, w.idx_in, s);
     if (e != hipSuccess) return e;
     ev.mark(2);
@@ -644,6 +649,8 @@ int ctg_rag_features(const void* labels, int label_bits, const void* data, int d
     }
     // record capacity: grows (and the scan re-runs) when exceeded
     int64_t need = std::max<int64_t>(w.rec.cap, std::max<int64_t>(1 << 16, V / 24));
+    need = (need + NREG - 1) / NREG * NREG;
+    RegionPrefix pre{};
     const bool stats = P.data_kind != CTG_DATA_NONE;
     for (int attempt = 0; attempt < 4; ++attempt) {
         CTG_CHECK(ensure_records(w, need, 0));
@@ -660,8 +667,20 @@ int ctg_rag_features(const void* labels, int label_bits, const void* data, int d
             return rag_dense_relabel(dl, dd, data_kind, n_channels, offsets, shape, own_begin, own_end,
                                      ignore_label, hist_lo, hist_hi, flags, stream, out);
         }
-        if ((int64_t)w.counters_host->n_records <= w.rec.cap) break;
-        need = (int64_t)(w.counters_host->n_records * 5 / 4) + 1024;
+        unsigned long long tot = 0, mx = 0;
+        for (int r = 0; r < NREG; ++r) {
+            pre.off[r] = (uint32_t)tot;
+            tot += w.counters_host->rcount[r];
+            mx = std::max(mx, w.counters_host->rcount[r]);
+        }
+        pre.off[NREG] = (uint32_t)tot;
+        w.counters_host->n_records = tot;
+        if (tot >= (1ull << 32)) {
+            set_error("ctg_rag_features: more than 2^32 records");
+            return CTG_ERR_NOMEM;
+        }
+        if ((int64_t)mx <= w.rec.rcap) break;
+        need = ((int64_t)(mx * 5 / 4) + 1024) * NREG;
         if (attempt == 3) {
             set_error("ctg_rag_features: record buffer overflow");
             return CTG_ERR_NOMEM;
@@ -681,6 +700,7 @@ int ctg_rag_features(const void* labels, int label_bits, const void* data, int d
     ReduceJob J{};
     J.n = n;
     J.keys = w.rec.key;
+    J.regions = &pre;
     J.R = w.rec;
     J.wide = 0;
     J.stats = stats;

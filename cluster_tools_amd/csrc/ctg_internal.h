@@ -67,11 +67,22 @@ __host__ __device__ inline uint32_t hash_key(uint64_t k) {
 // ---------------------------------------------------------------------------
 // records: the face scan flushes one record per (tile, edge)
 // ---------------------------------------------------------------------------
+// The scan reserves record slots from NREG region counters (region r owns
+// slots [r*rcap, (r+1)*rcap)) instead of one global counter: same-address
+// device atomics serialize (~25 ns each), and one counter per flush across
+// every workgroup of the chip was a measurable queue.
+constexpr int NREG = 64;
+
+struct RegionPrefix {          // exclusive prefix of the region counts (host-computed)
+    uint32_t off[NREG + 1];
+};
+
 struct RecordBuf {
     uint64_t* key = nullptr;      // (u << 32) | v
     double2* sums = nullptr;      // wide records: (sum, sum of squares); narrow: unused (in the body)
     uint32_t* hist = nullptr;     // narrow: NREC_STRIDE-word bodies; wide: WREC_WORDS per record
     int64_t cap = 0;
+    int64_t rcap = 0;             // slots per region (cap / NREG)
 };
 
 struct ScanParams {
@@ -104,6 +115,7 @@ struct Counters {               // device-side counters, zeroed per call
     unsigned long long label_overflow;  // labels >= 2^32 seen by the 32-bit key path
     unsigned long long max_v;        // largest label in any key
     unsigned long long pad[8];      // diagnostics (ablation checks, s_memtime stamps)
+    unsigned long long rcount[NREG];  // records reserved per region (may exceed rcap: overflow)
 };
 
 struct ReduceOut {

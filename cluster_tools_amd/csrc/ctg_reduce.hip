@@ -25,6 +25,20 @@ __global__ void k_pack_keys(int64_t n, const uint64_t* __restrict__ key, int nb,
     idx[i] = (uint32_t)i;
 }
 
+// scan records: region r holds pre.off[r+1]-pre.off[r] keys from slot r*rcap;
+// packed densely in region order, idx = the record's slot
+__global__ void k_pack_regions(const uint64_t* __restrict__ key, int64_t rcap, RegionPrefix pre, int nb,
+                               uint64_t* __restrict__ sk, uint32_t* __restrict__ idx) {
+    const int r = blockIdx.y;
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t b = pre.off[r];
+    if (i >= pre.off[r + 1] - b) return;
+    const uint64_t src = (uint64_t)r * (uint64_t)rcap + i;
+    const uint64_t k = key[src];
+    sk[b + i] = ((k >> 32) << nb) | (k & 0xFFFFFFFFull);
+    idx[b + i] = (uint32_t)src;
+}
+
 // pack (u,v) pairs given as two u64 (merge inputs); flags labels >= 2^32
 __global__ void k_pack_pairs(int64_t n, const uint64_t* __restrict__ uv, int nb, uint64_t* __restrict__ sk,
                              uint32_t* __restrict__ idx) {
@@ -460,6 +474,15 @@ hipError_t launch_gather_labels(const uint64_t* U, uint64_t* x, int64_t n, hipSt
 hipError_t launch_pack_keys(int64_t n, const uint64_t* key, int nb, uint64_t* sk, uint32_t* idx, hipStream_t s) {
     if (n == 0) return hipSuccess;
     hipLaunchKernelGGL(k_pack_keys, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, n, key, nb, sk, idx);
+    return hipGetLastError();
+}
+hipError_t launch_pack_regions(const uint64_t* key, int64_t rcap, const RegionPrefix& pre, int nb, uint64_t* sk,
+                               uint32_t* idx, hipStream_t s) {
+    uint32_t mx = 0;
+    for (int r = 0; r < NREG; ++r) mx = std::max(mx, pre.off[r + 1] - pre.off[r]);
+    if (mx == 0) return hipSuccess;
+    if ((uint64_t)rcap * NREG > (1ull << 32)) return hipErrorInvalidValue;   // slots index as u32
+    hipLaunchKernelGGL(k_pack_regions, dim3((mx + 255) / 256, NREG), dim3(256), 0, s, key, rcap, pre, nb, sk, idx);
     return hipGetLastError();
 }
 hipError_t launch_pack_pairs(int64_t n, const uint64_t* uv, int nb, uint64_t* sk, uint32_t* idx, hipStream_t s) {

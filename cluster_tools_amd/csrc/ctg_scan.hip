@@ -58,7 +58,11 @@ constexpr uint32_t WAVE_SAMPLE_BUDGET = 65535u / WAVES;
 #ifndef CTG_FILL_SOFT
 #define CTG_FILL_SOFT (TABLE_CAP / 2)
 #endif
-constexpr uint32_t FILL_SOFT = CTG_FILL_SOFT;             // request a flush past this many keys
+constexpr uint32_t FILL_SOFT = CTG_FILL_SOFT;
+// poll the flush request after every fold batch (1) or only at plane ends (0)
+#ifndef CTG_POLL_AFTER_FOLD
+#define CTG_POLL_AFTER_FOLD 1
+#endif             // request a flush past this many keys
 constexpr uint32_t MARK_ADJ = 0xFFFFFFFFu;                // stage entry: nearest-neighbour face, no sample
 constexpr uint32_t MARK_ONE = 0xFFFFFFFEu;                // stage entry: one affinity sample in .z
 
@@ -135,16 +139,15 @@ __device__ __noinline__ void table_flush(Table& T, RecordBuf R, Counters* C) {
     if (live) T.compact[off + rank] = (uint16_t)tid;
     if (tid == 0) T.ncompact = n;
     lds_barrier();
-    if (tid == 0 && n) {
-        T.base = atomicAdd(&C->n_records, (unsigned long long)n);
-        atomicMax(&C->max_v, T.maxv);
-    }
+    const int reg = blockIdx.x & (NREG - 1);
+    if (tid == 0 && n) T.base = atomicAdd(&C->rcount[reg], (unsigned long long)n);
     lds_barrier();
     if (n) {
         const unsigned long long base = T.base;
+        const unsigned long long rcap = (unsigned long long)R.rcap, slot0 = (unsigned long long)reg * rcap + base;
         for (uint32_t r = tid; r < n; r += SCAN_THREADS) {
             const int e = T.compact[r];
-            if (base + r < (unsigned long long)R.cap) R.key[base + r] = T.key[e];
+            if (base + r < rcap) R.key[slot0 + r] = T.key[e];
         }
         if (MODE != MODE_GRAPH) {
             // coalesced copy into the 128-byte record bodies
@@ -158,7 +161,7 @@ __device__ __noinline__ void table_flush(Table& T, RecordBuf R, Counters* C) {
                 } else if (j < NREC_OFF + NREC_WORDS) {
                     val = T.w[e][j - NREC_OFF];
                 }
-                if (base + r < (unsigned long long)R.cap) R.hist[(base + r) * NREC_STRIDE + j] = val;
+                if (base + r < rcap) R.hist[(slot0 + r) * NREC_STRIDE + j] = val;
             }
         }
         lds_barrier();
@@ -168,8 +171,70 @@ __device__ __noinline__ void table_flush(Table& T, RecordBuf R, Counters* C) {
     if (tid == 0) {
         T.used = 0;
         T.ncompact = 0;
-        T.maxv = 0;
         T.flush_req = 0;
+    }
+    lds_barrier();
+}
+
+#ifndef CTG_WAVE_FLUSH
+#define CTG_WAVE_FLUSH 1
+#endif
+// Flush by waves: every wave writes out the live entries among its own 64
+// table slots (entry tid) - its own record range from one global atomic, its
+// own 128-byte bodies, its own resets - so the flush needs two workgroup
+// barriers (table stable / table empty) instead of a workgroup-wide
+// compaction with one serial record reservation.
+template <int MODE>
+__device__ __noinline__ void table_flush_waves(Table& T, RecordBuf R, Counters* C) {
+    static_assert(TABLE_CAP == SCAN_THREADS, "one table entry per thread in the flush");
+    lds_barrier();
+    const int tid = threadIdx.x;
+    const int lane = tid & (WAVE - 1), wv = tid >> 6;
+    if (tid == 0) {   // no wave inserts or polls between the two barriers
+        T.used = 0;
+        T.flush_req = 0;
+    }
+    const uint64_t k = T.key[tid];
+    const bool live = k != EMPTY_KEY;
+    const uint64_t m = __ballot(live);
+    if (m) {
+        const uint32_t n = (uint32_t)__popcll(m);
+        const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+        uint32_t mv = live ? (uint32_t)k : 0u;
+        for (int o = 32; o > 0; o >>= 1) mv = max(mv, (uint32_t)__shfl_xor((int)mv, o, WAVE));
+        const int reg = (blockIdx.x * WAVES + wv) & (NREG - 1);
+        unsigned long long b = 0;
+        if (lane == 0) {
+            b = atomicAdd(&C->rcount[reg], (unsigned long long)n);
+            if (mv) atomicMax(&T.maxv, (unsigned long long)mv);
+        }
+        const unsigned long long base = ((unsigned long long)__builtin_amdgcn_readfirstlane((int)(b >> 32)) << 32) |
+                                        (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)b);
+        const unsigned long long rcap = (unsigned long long)R.rcap, slot0 = (unsigned long long)reg * rcap + base;
+        uint16_t* cw = T.compact + wv * WAVE;
+        if (live) {
+            if (base + rank < rcap) R.key[slot0 + rank] = k;
+            cw[rank] = (uint16_t)tid;
+        }
+        __builtin_amdgcn_wave_barrier();
+        if (MODE != MODE_GRAPH) {
+            // 16-byte pieces of the 128-byte bodies: piece q of record r
+            for (uint32_t f = lane; f < n * 8; f += WAVE) {
+                const uint32_t r = f >> 3, q = f & 7;
+                const int e = cw[r];
+                uint4 val = make_uint4(0u, 0u, 0u, 0u);
+                if (q == 0) {
+                    const double2 sq2 = make_double2(T.sum[e], T.sq[e]);
+                    val = *reinterpret_cast<const uint4*>(&sq2);
+                } else if (q < 7) {
+                    const uint32_t* w = &T.w[e][4 * (q - 1)];
+                    val = make_uint4(w[0], w[1], w[2], w[3]);
+                }
+                if (base + r < rcap) reinterpret_cast<uint4*>(R.hist + (slot0 + r) * NREC_STRIDE)[q] = val;
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+        if (live) entry_reset(T, tid);
     }
     lds_barrier();
 }
@@ -179,10 +244,12 @@ __device__ __noinline__ void table_flush(Table& T, RecordBuf R, Counters* C) {
 // sum, sum of squares and ordered min / max this record carries.
 __device__ __noinline__ void emit_direct(RecordBuf R, Counters* C, uint64_t key, uint32_t cnt_flag, int sa, int sb,
                                          double s, double q, uint32_t mn, uint32_t mx, bool with_stats) {
-    unsigned long long i = atomicAdd(&C->n_records, 1ull);
+    const int reg = blockIdx.x & (NREG - 1);
+    const unsigned long long j = atomicAdd(&C->rcount[reg], 1ull);
     atomicAdd(&C->n_direct, 1ull);
     atomicMax(&C->max_v, (unsigned long long)(key & 0xFFFFFFFFull));
-    if (i >= (unsigned long long)R.cap) return;
+    if (j >= (unsigned long long)R.rcap) return;
+    const unsigned long long i = (unsigned long long)reg * (unsigned long long)R.rcap + j;
     R.key[i] = key;
     if (!with_stats) return;
     uint32_t* b = R.hist + i * NREC_STRIDE;
@@ -399,6 +466,12 @@ __device__ __forceinline__ uint32_t shl1(uint32_t v, uint32_t edge) {
     return (uint32_t)__builtin_amdgcn_update_dpp((int)edge, (int)v, 0x130, 0xf, 0xf, false);
 }
 
+#if CTG_WAVE_FLUSH
+#define FLUSH_TABLE table_flush_waves
+#else
+#define FLUSH_TABLE table_flush
+#endif
+
 template <typename LabelT, typename DataT, int MODE, bool FAST40>
 __global__ __launch_bounds__(SCAN_THREADS, 4) void k_face_scan(ScanParams P, RecordBuf R, Counters* C) {
     constexpr bool BND = MODE == MODE_BOUNDARY;
@@ -529,7 +602,7 @@ __global__ __launch_bounds__(SCAN_THREADS, 4) void k_face_scan(ScanParams P, Rec
             (int)__hip_atomic_load(&T.flush_req, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
         if (fr) {
             const uint64_t t0 = stamps ? stamp_now() : 0;
-            table_flush<MODE>(T, R, C);
+            FLUSH_TABLE<MODE>(T, R, C);
             wsamp = 0;
             if (stamps) t_flush += stamp_now() - t0;
         }
@@ -549,7 +622,9 @@ __global__ __launch_bounds__(SCAN_THREADS, 4) void k_face_scan(ScanParams P, Rec
             fold_batch<MODE, FAST40, StageT, NPER>(T, stage, nbuf, lane, R, C, scale, offset, need, ablate);
             nbuf = 0;
             if (stamps) t_fold += stamp_now() - t0;
+#if CTG_POLL_AFTER_FOLD
             poll();
+#endif
         }
     };
     // append the active lanes of one site to the stage
@@ -662,7 +737,7 @@ __global__ __launch_bounds__(SCAN_THREADS, 4) void k_face_scan(ScanParams P, Rec
         const uint32_t fr = (uint32_t)__builtin_amdgcn_readfirstlane(
             (int)__hip_atomic_load(&T.flush_req, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
         if (fr) {
-            table_flush<MODE>(T, R, C);
+            FLUSH_TABLE<MODE>(T, R, C);
             continue;
         }
         const uint32_t lv = (uint32_t)__builtin_amdgcn_readfirstlane(
@@ -670,7 +745,8 @@ __global__ __launch_bounds__(SCAN_THREADS, 4) void k_face_scan(ScanParams P, Rec
         if (lv == 0) break;
         __builtin_amdgcn_s_sleep(2);
     }
-    table_flush<MODE>(T, R, C);
+    FLUSH_TABLE<MODE>(T, R, C);
+    if (tid == 0 && T.maxv) atomicMax(&C->max_v, T.maxv);   // after the final flush's barrier
     if (stamps && lane == 0) {
         atomicAdd(&C->pad[2], (unsigned long long)(stamp_now() - t_start));
         atomicAdd(&C->pad[3], (unsigned long long)t_fold);
