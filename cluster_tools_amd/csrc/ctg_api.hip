@@ -191,6 +191,30 @@ struct Ev {
         if (e_ != hipSuccess) return e_;                          \
     } while (0)
 
+// Record sort: (u,v) keys packed to 2*nb bits (34 at 1.3e5 labels).  rocPRIM's
+// gfx950 default sorts 8 bits per onesweep pass (5 passes at 34 bits, each a
+// launch with its own decoupled look-back); 10-bit digits cut that to 4 (34 bits)
+// and the sort from 0.185 to 0.151 ms at 512^3 (11+ bits exceed the LDS of the
+// histogram kernel).
+#ifndef CTG_SORT_BITS
+#define CTG_SORT_BITS 10
+#endif
+#ifndef CTG_SORT_BLOCK
+#define CTG_SORT_BLOCK 1024
+#endif
+#ifndef CTG_SORT_IPT
+#define CTG_SORT_IPT 8
+#endif
+#if CTG_SORT_BITS
+using RecordSortConfig = rocprim::radix_sort_config<
+    rocprim::default_config, rocprim::default_config,
+    rocprim::radix_sort_onesweep_config<rocprim::kernel_config<256, 16>,
+                                        rocprim::kernel_config<CTG_SORT_BLOCK, CTG_SORT_IPT>, CTG_SORT_BITS,
+                                        rocprim::block_radix_rank_algorithm::match>>;
+#else
+using RecordSortConfig = rocprim::default_config;
+#endif
+
 // ---------------------------------------------------------------------------
 // shared back half: records (n, with keys (u<<32|v) or (u,v) pairs) -> result
 // ---------------------------------------------------------------------------
@@ -258,8 +282,8 @@ static hipError_t reduce_records(Workspace& w, const ReduceJob& J, hipStream_t s
     else e = launch_pack_pairs(n, J.pairs, nb, w.sk_in, w.idx_in, s);
     if (e != hipSuccess) return e;
     ev.mark(2);
-    ROCPRIM_CALL(w, rocprim::radix_sort_pairs(t, tbytes, w.sk_in, w.sk_out, w.idx_in, w.idx_out, (size_t)n, 0u,
-                                              (unsigned)(2 * nb), s));
+    ROCPRIM_CALL(w, rocprim::radix_sort_pairs<RecordSortConfig>(t, tbytes, w.sk_in, w.sk_out, w.idx_in, w.idx_out,
+                                                                (size_t)n, 0u, (unsigned)(2 * nb), s));
     ev.mark(3);
     ROCPRIM_CALL(w, rocprim::run_length_encode(t, tbytes, w.sk_out, (unsigned)n, w.uniq, w.runs, dE_all, s));
     // offsets over the n-bound: entries past E_all are never read
