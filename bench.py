@@ -61,6 +61,11 @@ def parse():
     p.add_argument('--cpu-baseline-planes', type=int, default=96,
                    help='z-planes of the per-GPU volume timed with the C oracle (0 = skip)')
     p.add_argument('--no-cpu-baseline', action='store_true')
+    # rehearsal of the N>1 path on a one-GPU box: every rank on one device,
+    # exchange over gloo (the driver's multi-GPU runs use the defaults: RCCL,
+    # device = LOCAL_RANK)
+    p.add_argument('--backend', default='nccl', choices=['nccl', 'gloo'])
+    p.add_argument('--device', type=int, default=None)
     return p.parse_args()
 
 
@@ -104,14 +109,18 @@ def main():
     local = int(os.environ.get('LOCAL_RANK', '0'))
     if args.gpus != world and world > 1:
         print('warning: --gpus %d but WORLD_SIZE %d' % (args.gpus, world), file=sys.stderr)
-    torch.cuda.set_device(local)
+    dev = local if args.device is None else args.device
+    torch.cuda.set_device(dev)
     if world > 1:
-        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+        if args.backend == 'nccl':
+            dist.init_process_group('nccl', device_id=torch.device('cuda', dev))
+        else:
+            dist.init_process_group('gloo')
 
     from cluster_tools_amd import rag
     from cluster_tools_amd import _lib
 
-    _lib.init_device(local)
+    _lib.init_device(dev)
     S0, cell0, aff, scaling, label = WORKLOADS[args.config]
     S = args.size or S0
     cell = args.cell or cell0
@@ -172,7 +181,7 @@ def main():
     rag.set_profiling(False)
     elapsed = t1 - t0
     if world > 1:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device='cuda')
+        tt = torch.tensor([elapsed], dtype=torch.float64, device='cuda' if args.backend == 'nccl' else 'cpu')
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
     n_edges_local = res.n_edges
@@ -185,7 +194,7 @@ def main():
     value = total_vox / (elapsed / args.steps) / 1e9
     n_edges = n_edges_local
     if world > 1:
-        te = torch.tensor([n_edges_local], dtype=torch.int64, device='cuda')
+        te = torch.tensor([n_edges_local], dtype=torch.int64, device='cuda' if args.backend == 'nccl' else 'cpu')
         dist.all_reduce(te)
         n_edges = int(te.item())
 
