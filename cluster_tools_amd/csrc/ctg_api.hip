@@ -214,6 +214,18 @@ using RecordSortConfig = rocprim::radix_sort_config<
 #else
 using RecordSortConfig = rocprim::default_config;
 #endif
+// The wide digits pay off for small sorts (launch / look-back bound: 1.9 M
+// records at 512^3: 0.185 -> 0.151 ms; 27.8 M at 2048^3: 1.88 -> 1.49 ms) and
+// lose for very large ones (298 M records of configs[4]:
+// 14.1 -> 18.7 ms, the 1024-way scatter coalesces worse), so they are used up
+// to this many records (CTG_SORT_WIDE_MAX overrides).
+static int64_t sort_wide_digits_max() {
+    static const int64_t v = [] {
+        const char* e = getenv("CTG_SORT_WIDE_MAX");
+        return e ? (int64_t)atoll(e) : (int64_t)(64 << 20);
+    }();
+    return v;
+}
 
 // ---------------------------------------------------------------------------
 // shared back half: records (n, with keys (u<<32|v) or (u,v) pairs) -> result
@@ -282,8 +294,13 @@ static hipError_t reduce_records(Workspace& w, const ReduceJob& J, hipStream_t s
     else e = launch_pack_pairs(n, J.pairs, nb, w.sk_in, w.idx_in, s);
     if (e != hipSuccess) return e;
     ev.mark(2);
-    ROCPRIM_CALL(w, rocprim::radix_sort_pairs<RecordSortConfig>(t, tbytes, w.sk_in, w.sk_out, w.idx_in, w.idx_out,
-                                                                (size_t)n, 0u, (unsigned)(2 * nb), s));
+    if (n <= sort_wide_digits_max()) {
+        ROCPRIM_CALL(w, rocprim::radix_sort_pairs<RecordSortConfig>(t, tbytes, w.sk_in, w.sk_out, w.idx_in,
+                                                                    w.idx_out, (size_t)n, 0u, (unsigned)(2 * nb), s));
+    } else {
+        ROCPRIM_CALL(w, rocprim::radix_sort_pairs(t, tbytes, w.sk_in, w.sk_out, w.idx_in, w.idx_out, (size_t)n, 0u,
+                                                  (unsigned)(2 * nb), s));
+    }
     ev.mark(3);
     ROCPRIM_CALL(w, rocprim::run_length_encode(t, tbytes, w.sk_out, (unsigned)n, w.uniq, w.runs, dE_all, s));
     // offsets over the n-bound: entries past E_all are never read
@@ -301,6 +318,7 @@ static hipError_t reduce_records(Workspace& w, const ReduceJob& J, hipStream_t s
         O.wsums = (double2*)dalloc(n * 16);
     }
     if (!O.edges || (J.stats && !O.feats)) return hipErrorOutOfMemory;
+    O.count_out = may_drop ? nullptr : dE;   // no compaction: the kernel copies the count
     e = launch_reduce(n, dE_all, w.uniq, w.runs, w.offs, w.idx_out, J.R, J.wide, J.stats, nb, J.need_adj,
                       J.ignore_label, J.scale, J.offset, O, s);
     if (e != hipSuccess) return e;
@@ -317,9 +335,6 @@ static hipError_t reduce_records(Workspace& w, const ReduceJob& J, hipStream_t s
         if (e != hipSuccess) return e;
         dfree(O.edges); dfree(O.feats); dfree(O.wstats); dfree(O.wsums);   // stream-ordered reuse
         O = C2;
-    } else {
-        e = hipMemcpyAsync(dE, dE_all, 4, hipMemcpyDeviceToDevice, s);
-        if (e != hipSuccess) return e;
     }
     ev.mark(5);
     res->edges = O.edges;

@@ -124,6 +124,7 @@ struct ReduceOut {
     uint32_t* keep;       // E or null
     uint32_t* wstats;     // WREC_WORDS*E or null
     double2* wsums;       // E or null
+    uint32_t* count_out;  // null, or receives the edge count (no compaction follows)
 };
 
 struct Workspace {

@@ -182,6 +182,7 @@ __global__ __launch_bounds__(256) void k_reduce_edges(int64_t E, const uint32_t*
                                                       int need_adj, int ignore_label, double scale, double offset,
                                                       ReduceOut O) {
     const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e == 0 && O.count_out) *O.count_out = *dE;
     if (e >= E || e >= (int64_t)*dE) return;
     const uint64_t sk = uniq[e];
     const uint64_t u = sk >> nb, v = sk & ((1ull << nb) - 1ull);
