@@ -663,6 +663,20 @@ int ctg_rag_features(const void* labels, int label_bits, const void* data, int d
             P.adj_mask = cap - 1;
         }
     }
+    {
+        bool nn[3] = {false, false, false};
+        for (int c = 0; c < P.n_channels; ++c) {
+            const int* o = P.offsets[c];
+            if (std::abs(o[0]) + std::abs(o[1]) + std::abs(o[2]) > 1) P.lr_mask |= 1u << c;
+            for (int a = 0; a < 3; ++a)
+                nn[a] |= o[a] == -1 && o[(a + 1) % 3] == 0 && o[(a + 2) % 3] == 0;
+        }
+        // every nearest-neighbour face yields a sample of its channel, and the
+        // long-range samples are filtered in the scan: all keys are RAG edges
+        P.skip_adj_marks = P.n_channels > 0 && nn[0] && nn[1] && nn[2] && !(flags & CTG_NO_ADJ_FILTER) &&
+                           (!long_range || P.adj_set != nullptr);
+        if (const char* sa = getenv("CTG_SKIP_ADJ")) P.skip_adj_marks = P.skip_adj_marks && atoi(sa);
+    }
     struct AdjRelease {   // the set and its graph live until the scan is done
         unsigned long long*& set;
         ctg_result*& g;
@@ -743,7 +757,7 @@ int ctg_rag_features(const void* labels, int label_bits, const void* data, int d
     J.R = w.rec;
     J.wide = 0;
     J.stats = stats;
-    J.need_adj = P.n_channels > 0 ? ((flags & CTG_NO_ADJ_FILTER) ? 2 : 1) : 0;
+    J.need_adj = P.n_channels > 0 && !P.skip_adj_marks ? ((flags & CTG_NO_ADJ_FILTER) ? 2 : 1) : 0;
     J.ignore_label = ignore_label;
     J.keep_stats = (flags & CTG_KEEP_STATS) ? 1 : 0;
     J.max_v = w.counters_host->max_v;

@@ -107,6 +107,11 @@ struct ScanParams {
     uint32_t adj_mask;         // set capacity - 1 (power of two)
     int64_t ntiles[3];         // tiles along x, y, z (set by the launcher)
     int xcd_remap;             // 1: XCD-contiguous tile order (see k_face_scan)
+    // affinities: the three nearest-neighbour channels are present and every
+    // long-range sample is filtered against the RAG edge set, so every table
+    // key is a RAG edge and the scan pushes no adjacency markers
+    int skip_adj_marks;
+    uint32_t lr_mask;          // bit c: channel c is long-range (|offset|_1 > 1)
 };
 
 struct Counters {               // device-side counters, zeroed per call

@@ -63,6 +63,13 @@ constexpr uint32_t FILL_SOFT = CTG_FILL_SOFT;
 #ifndef CTG_POLL_AFTER_FOLD
 #define CTG_POLL_AFTER_FOLD 1
 #endif             // request a flush past this many keys
+#ifndef CTG_CG
+#define CTG_CG 1
+#endif
+// affinity channels per load group: 1 measured best (3 nearest-neighbour
+// channels 13.3 ms scan at 1024^3 vs 16.7 ms with 4; 12 channels equal - that
+// case is bound by folding ~5 samples per voxel, not by load latency)
+constexpr int CG = CTG_CG;
 constexpr uint32_t MARK_ADJ = 0xFFFFFFFFu;                // stage entry: nearest-neighbour face, no sample
 constexpr uint32_t MARK_ONE = 0xFFFFFFFEu;                // stage entry: one affinity sample in .z
 
@@ -442,8 +449,8 @@ __device__ __forceinline__ void fold_batch(Table& T, const StageT* __restrict__ 
 }
 
 // membership of an edge key in the RAG edge set (linear probing, load <= 1/2)
-__device__ __forceinline__ bool adj_contains(const unsigned long long* __restrict__ set, uint32_t mask, uint64_t key) {
-    uint32_t h = hash_key(key) & mask;
+__device__ __forceinline__ bool adj_contains(const unsigned long long* __restrict__ set, uint32_t mask, uint64_t key,
+                                             uint32_t h) {
 #pragma unroll 1
     for (;;) {
         const unsigned long long k = set[h];
@@ -540,6 +547,7 @@ __global__ __launch_bounds__(SCAN_THREADS, 4) void k_face_scan(ScanParams P, Rec
         if (y < Y && y >= oby && y < oey) row_x |= 1u << r;
         if (y + 1 < Y && y + 1 >= oby && y + 1 < oey) row_y |= 1u << r;
     }
+    const bool adj_marks = AFF && !P.skip_adj_marks;   // push nearest-neighbour adjacency markers
     const int xh = x0 + TILE_X;              // x of the lane-63 neighbour
     const bool has_xh = xh < X;
 
@@ -663,7 +671,7 @@ __global__ __launch_bounds__(SCAN_THREADS, 4) void k_face_scan(ScanParams P, Rec
                 const uint32_t lc = Lc[r];
                 // x face (x, x+1); lane 63 takes its neighbour from the x-halo
                 const uint32_t lx = shl1(lc, (uint32_t)__builtin_amdgcn_readlane((int)XLc, r));
-                if (zlo && (row_x >> r & 1u)) {
+                if (zlo && (row_x >> r & 1u) && (!AFF || adj_marks)) {
                     const float dx = BND ? __uint_as_float(shl1(__float_as_uint(Dc[r]),
                                                                 (uint32_t)__builtin_amdgcn_readlane(
                                                                     (int)__float_as_uint(XDc), r)))
@@ -671,7 +679,7 @@ __global__ __launch_bounds__(SCAN_THREADS, 4) void k_face_scan(ScanParams P, Rec
                     push(lane_xf && lc != lx, lc, lx, __float_as_uint(Dc[r]), AFF ? MARK_ADJ : __float_as_uint(dx));
                 }
                 // y face (y, y+1)
-                if (zlo && (row_y >> r & 1u))
+                if (zlo && (row_y >> r & 1u) && (!AFF || adj_marks))
                     push(lane_yz && lc != Lc[r + 1], lc, Lc[r + 1], __float_as_uint(Dc[r]),
                          AFF ? MARK_ADJ : __float_as_uint(Dc[r + 1]));
                 // affinity samples aff[c, p] for q = p + o_c, p in the owned box
@@ -679,25 +687,53 @@ __global__ __launch_bounds__(SCAN_THREADS, 4) void k_face_scan(ScanParams P, Rec
                     const int y = yw + r;
                     if (zlo && (row_x >> r & 1u)) {
                         const int64_t i = (int64_t)z * sz + (int64_t)y * X + x;
-                        for (int c = 0; c < P.n_channels; ++c) {
-                            const int qz = z + P.offsets[c][0];
-                            const int qy = y + P.offsets[c][1];
-                            const int qx = x + P.offsets[c][2];
-                            const bool inq = lane_yz && qz >= 0 && qz < Z && qy >= 0 && qy < Y && qx >= 0 && qx < X;
-                            uint32_t lq = lc;
-                            float av = 0.f;
-                            if (inq) {
-                                lq = narrow(L[(int64_t)qz * sz + (int64_t)qy * X + qx]);
-                                av = load_val<DataT>(D, (int64_t)c * Z * sz + i);
+                        // channels in groups of CG: the group's label gathers,
+                        // sample loads and first edge-set probes are in flight
+                        // together instead of one round trip per channel
+                        for (int c0 = 0; c0 < P.n_channels; c0 += CG) {
+                            uint32_t lq[CG];
+                            float av[CG];
+                            bool act[CG];
+#pragma unroll
+                            for (int j = 0; j < CG; ++j) {
+                                const int c = c0 + j;
+                                lq[j] = lc;
+                                av[j] = 0.f;
+                                act[j] = false;
+                                if (c < P.n_channels) {
+                                    const int qz = z + P.offsets[c][0];
+                                    const int qy = y + P.offsets[c][1];
+                                    const int qx = x + P.offsets[c][2];
+                                    act[j] = lane_yz && qz >= 0 && qz < Z && qy >= 0 && qy < Y && qx >= 0 && qx < X;
+                                    if (act[j]) {
+                                        lq[j] = narrow(L[(int64_t)qz * sz + (int64_t)qy * X + qx]);
+                                        av[j] = load_val<DataT>(D, (int64_t)c * Z * sz + i);
+                                    }
+                                }
                             }
-                            bool act = inq && lq != lc;
-                            // long-range channel: only pairs that are RAG edges
-                            if (P.adj_set != nullptr && (abs(P.offsets[c][0]) + abs(P.offsets[c][1]) +
-                                                             abs(P.offsets[c][2])) > 1) {
-                                if (act) act = adj_contains(P.adj_set, P.adj_mask,
-                                                            ((uint64_t)min(lc, lq) << 32) | max(lc, lq));
+#pragma unroll
+                            for (int j = 0; j < CG; ++j) act[j] = act[j] && lq[j] != lc;
+                            // long-range channels: only pairs that are RAG edges
+                            if (P.adj_set != nullptr && ((P.lr_mask >> c0) & ((1u << CG) - 1u))) {
+                                uint64_t key[CG];
+                                unsigned long long k0[CG];
+                                bool lr[CG];
+#pragma unroll
+                                for (int j = 0; j < CG; ++j) {
+                                    lr[j] = act[j] && ((P.lr_mask >> (c0 + j)) & 1u);
+                                    key[j] = ((uint64_t)min(lc, lq[j]) << 32) | max(lc, lq[j]);
+                                    k0[j] = lr[j] ? P.adj_set[hash_key(key[j]) & P.adj_mask] : EMPTY_KEY;
+                                }
+#pragma unroll
+                                for (int j = 0; j < CG; ++j)
+                                    if (lr[j] && k0[j] != key[j])
+                                        act[j] = k0[j] != EMPTY_KEY &&
+                                                 adj_contains(P.adj_set, P.adj_mask, key[j],
+                                                              (hash_key(key[j]) + 1u) & P.adj_mask);
                             }
-                            push(act, lc, lq, __float_as_uint(av), MARK_ONE);
+#pragma unroll
+                            for (int j = 0; j < CG; ++j)
+                                if (c0 + j < P.n_channels) push(act[j], lc, lq[j], __float_as_uint(av[j]), MARK_ONE);
                         }
                     }
                 }
@@ -708,7 +744,7 @@ __global__ __launch_bounds__(SCAN_THREADS, 4) void k_face_scan(ScanParams P, Rec
                 __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): the prefetched plane has landed
                 t_wait += stamp_now() - t0;
             }
-            if (zup) {
+            if (zup && (!AFF || adj_marks)) {
 #pragma unroll
                 for (int r = 0; r < ROWS; ++r) {
                     const uint32_t ln = (uint32_t)Ln[r];
