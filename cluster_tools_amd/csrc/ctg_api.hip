@@ -701,6 +701,11 @@ int ctg_rag_features(const void* labels, int label_bits, const void* data, int d
         return CTG_OK;
     }
     // record capacity: grows (and the scan re-runs) when exceeded
+    if (getenv("CTG_REC_FRESH")) {   // test hook: start from the smallest record buffer
+        CTG_CHECK(hipStreamSynchronize(s));
+        dfree(w.rec.key); dfree(w.rec.sums); dfree(w.rec.hist);
+        w.rec = RecordBuf{};
+    }
     int64_t need = std::max<int64_t>(w.rec.cap, std::max<int64_t>(1 << 16, V / 24));
     need = (need + NREG - 1) / NREG * NREG;
     RegionPrefix pre{};

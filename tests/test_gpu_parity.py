@@ -256,6 +256,53 @@ def test_affinity_random_volumes(gpu, offsets):
     check_features(out['features'], f_ref)
 
 
+@pytest.mark.parametrize('offsets', [
+    [[-1, 0, 0], [0, -1, 0], [0, 0, -3]],                 # one nearest-neighbour channel missing
+    [[0, 0, -1], [-1, 0, 0], [0, -1, 0], [0, 0, -9]],      # nearest-neighbour channels in another order
+    [[-2, 0, 0], [0, -3, 0]],                              # long-range channels only
+])
+def test_affinity_channel_sets(gpu, offsets):
+    """Channel sets with and without the three nearest-neighbour offsets: the
+    scan pushes adjacency markers only when they are not all present."""
+    lab, bnd = S.generate((18, 50, 70), cell=6, seed=21)
+    affs = S.affinities_from_boundary(bnd, offsets)
+    e_ref, f_ref = O.affinity_features(lab, affs, offsets)
+    out = rag.rag_features(lab, affs, offsets=offsets)
+    np.testing.assert_array_equal(out['edges'], e_ref)
+    check_features(out['features'], f_ref)
+
+
+def test_affinity_without_marker_skip_is_identical(gpu, monkeypatch):
+    """CTG_SKIP_ADJ=0 forces the adjacency markers: same edges, same features."""
+    lab, bnd = S.generate((18, 50, 70), cell=6, seed=22)
+    for offs in (S.NN_OFFSETS, S.LR_OFFSETS):
+        affs = S.affinities_from_boundary(bnd, offs)
+        a = rag.rag_features(lab, affs, offsets=offs)
+        monkeypatch.setenv('CTG_SKIP_ADJ', '0')
+        b = rag.rag_features(lab, affs, offsets=offs)
+        monkeypatch.delenv('CTG_SKIP_ADJ')
+        np.testing.assert_array_equal(a['edges'], b['edges'])
+        np.testing.assert_array_equal(a['nodes'], b['nodes'])
+        np.testing.assert_array_equal(a['features'][:, 9], b['features'][:, 9])
+        np.testing.assert_allclose(a['features'], b['features'], rtol=1e-12, atol=1e-12)
+
+
+def test_record_regions_overflow(gpu, monkeypatch):
+    """Smallest record buffer (CTG_REC_FRESH: 64 regions of 1024 slots) on
+    random labels: the regions overflow and the scan re-runs with a larger
+    buffer; the result must still match the oracle."""
+    rng = np.random.default_rng(5)
+    lab = rng.integers(0, 200000, size=(16, 48, 96)).astype(np.uint64)
+    bnd = rng.random(lab.shape).astype(np.float32)
+    monkeypatch.setenv('CTG_REC_FRESH', '1')
+    out = rag.rag_features(lab, bnd)
+    monkeypatch.delenv('CTG_REC_FRESH')
+    e_ref, f_ref = O.boundary_features(lab, bnd)
+    assert e_ref.shape[0] > 64 * 1024
+    np.testing.assert_array_equal(out['edges'], e_ref)
+    check_features(out['features'], f_ref)
+
+
 def test_affinity_edge_list_filter(gpu):
     """no_adj_filter + an explicit edge list = the ndist per-block semantics."""
     lab, bnd = S.generate((16, 40, 40), cell=5, seed=13)
