@@ -69,3 +69,17 @@ def features(labels, data=None, offsets=None, own_begin=None, ignore_label=False
     lib.ctgo_free(ep)
     lib.ctgo_free(fp)
     return edges, feats
+
+
+def chunk_job(args):
+    """One z-chunk of a slab stored as .npy files (bench.py's CPU baseline):
+    (labels_path, data_path, z0, z1, halo) -> (n_edges, seconds of the C call).
+    The chunk is read from the memory-mapped files before the clock starts."""
+    import time
+    lp, dp, z0, z1, halo = args
+    lab = np.ascontiguousarray(np.load(lp, mmap_mode='r')[z0 - halo:z1])
+    dat = np.ascontiguousarray(np.load(dp, mmap_mode='r')[z0 - halo:z1])
+    load()
+    t0 = time.perf_counter()
+    e, _ = features(lab, dat, own_begin=(halo, 0, 0))
+    return int(e.shape[0]), time.perf_counter() - t0
