@@ -159,6 +159,23 @@ def _pack_uv(k):
     return k[:, 0] * (1 << 32) + k[:, 1]
 
 
+def _merge_sorted(ka, fa, kb, fb):
+    """Merge two (u,v)-sorted row sets with disjoint keys (the local-only rows
+    and the merged shared rows) by scatter, not a sort of the whole shard."""
+    pa, pb = _pack_uv(ka), _pack_uv(kb)
+    na, nb = pa.shape[0], pb.shape[0]
+    dev = ka.device
+    pos_a = torch.arange(na, device=dev) + torch.searchsorted(pb, pa)
+    pos_b = torch.arange(nb, device=dev) + torch.searchsorted(pa, pb)
+    k = torch.empty((na + nb,) + tuple(ka.shape[1:]), dtype=ka.dtype, device=dev)
+    f = torch.empty((na + nb,) + tuple(fa.shape[1:]), dtype=fa.dtype, device=dev)
+    k[pos_a] = ka
+    k[pos_b] = kb
+    f[pos_a] = fa
+    f[pos_b] = fb
+    return {'edges': k, 'features': f}
+
+
 def _tensor(x, like):
     if isinstance(x, torch.Tensor):
         return x
@@ -203,12 +220,12 @@ class DistResult:
         self.merged = {'edges': self.merged['edges'][:0], 'features': self.merged['features'][:0]}
 
 
-def _exclusive_offset(n_local, group, device):
-    t = torch.tensor([n_local], dtype=torch.int64, device=device)
-    allc = all_gather_tensor(t, group)
-    counts = [int(x.item()) for x in allc]
+def _exclusive_offsets(n_locals, group, device):
+    """[(offset of this rank, total)] for each local count, one all_gather."""
+    t = torch.tensor(list(n_locals), dtype=torch.int64, device=device)
+    allc = torch.stack(all_gather_tensor(t, group)).cpu().tolist()
     r = dist.get_rank(group)
-    return sum(counts[:r]), sum(counts)
+    return [(sum(row[k] for row in allc[:r]), sum(row[k] for row in allc)) for k in range(len(n_locals))]
 
 
 def rag_features_distributed(labels, data=None, offsets=None, own_begin=None, own_end=None,
@@ -277,16 +294,12 @@ def rag_features_distributed(labels, data=None, offsets=None, own_begin=None, ow
                                    torch.cat([rr, lr[shared]]), hist_range)
             me = _tensor(me, lk)
             mf = _tensor(mf, lf)
-            ak = torch.cat([lk[keep], me])
-            af = torch.cat([lf[keep], mf])
-            order = torch.argsort(_pack_uv(ak))
-            merged = {'edges': ak[order], 'features': af[order]}
+            merged = _merge_sorted(lk[keep], lf[keep], me, mf)
     n_loc = int(merged['edges'].shape[0])
 
     # nodes -> the same ranges
     nrecv = exchange(nodes.reshape(-1), split_counts(nodes.reshape(-1), splitters), group)
     node_shard = backend.unique(nrecv)
 
-    e_off, e_tot = _exclusive_offset(n_loc, group, dev)
-    n_off, n_tot = _exclusive_offset(int(node_shard.shape[0]), group, dev)
+    (e_off, e_tot), (n_off, n_tot) = _exclusive_offsets([n_loc, int(node_shard.shape[0])], group, dev)
     return DistResult(merged, node_shard, e_off, e_tot, n_off, n_tot, info)
