@@ -158,3 +158,26 @@ def test_blocking_neighbor_ids():
     assert b.getNeighborId(bid, 0, False) == -1
     assert b.getNeighborId(bid, 1, True) == -1
     assert b.getNeighborId(bid, 2, False) == b.gridPositionToBlockId([1, 0, 2])
+
+
+def test_bench_cpu_baseline_chunks_cover_the_slab():
+    """bench.py's CPU baseline: z-chunks with a halo plane, faces owned by the
+    upper voxel, so the chunk edge sets together are the slab's RAG."""
+    import os
+    import sys
+    torch = pytest.importorskip('torch')
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    lab, bnd = S.generate((24, 40, 56), cell=6, seed=4)
+    v, info = bench.cpu_baseline(torch.from_numpy(lab.view(np.int64)), torch.from_numpy(bnd), 24, 3)
+    assert v > 0 and info['threads'] == 3
+    from oracle import c_oracle
+    whole, _ = c_oracle.features(lab, bnd)
+    parts = []
+    for z0, z1 in ((0, 8), (8, 16), (16, 24)):
+        h = 1 if z0 else 0
+        e, _ = c_oracle.features(lab[z0 - h:z1], bnd[z0 - h:z1], own_begin=(h, 0, 0))
+        parts.append(e)
+    u = np.unique(np.concatenate(parts), axis=0)
+    np.testing.assert_array_equal(u, whole)
+    assert '3 z-chunks on 3 worker processes' in info['sample']
