@@ -15,6 +15,7 @@ whole integration:
     extractBlockFeaturesFromAffinityMaps_{float32,uint8}
                                    features/block_edge_features.py:138-145
     mergeFeatureBlocks             features/merge_edge_features.py:141-147
+    serializeMergedGraph           multicut/reduce_problem.py:247-258
     Graph                          test/graph/test_graph.py:32,68,111;
                                    multicut/solve_subproblems.py:250
 
@@ -144,6 +145,76 @@ def mergeSubgraphs(graphPath, subgraphKey, blockIds, outKey, numberOfThreads=1, 
             ds_e[:] = edges
         out.attrs['numberOfNodes'] = n_nodes
         out.attrs['numberOfEdges'] = n_edges
+
+
+def serializeMergedGraph(graphPath, graphBlockPrefix, shape, blockShape, newBlockShape, newBlockIds,  # noqa: N802,N803
+                         nodeLabeling, edgeLabeling, outPath, graphOutPrefix, numberOfThreads=1,  # noqa: N803
+                         serializeEdges=True):  # noqa: N803
+    """Sub-graphs of the next (coarser) scale of the blockwise multicut
+    (multicut/reduce_problem.py:247-258, lifted_multicut/reduce_lifted_problem.py:256).
+
+    For every new block: the old-scale blocks inside it (``blockShape`` grid
+    under ``graphBlockPrefix``) are united, their nodes mapped through
+    ``nodeLabeling`` (dense, old node id -> new node id, reduce_problem.py:165-193)
+    and written as the sorted unique varlen ``nodes`` chunk of
+    ``graphOutPrefix`` at the new block's grid position -- the chunk
+    solve_subproblems.py:135-136 reads at the next scale.  With
+    ``serializeEdges`` the old block edges are mapped the same way, edges that
+    collapse to one node are dropped, and the sorted unique ``edges`` chunk
+    (flattened (u, v)) is written, plus ``edge_ids`` = ``edgeLabeling`` of the
+    old global ids when the old scale has ``edge_ids`` chunks.  The reference
+    only calls this with serializeEdges=False; the edge branch follows the
+    same rule and is parity unpinned (nifty is not available).
+    """
+    node_lab = np.asarray(nodeLabeling, dtype=np.uint64)
+    edge_lab = None if edgeLabeling is None else np.asarray(edgeLabeling, dtype=np.uint64)
+    shape = [int(s) for s in shape]
+    old_blk = blocking([0, 0, 0], shape, [int(b) for b in blockShape])
+    new_blk = blocking([0, 0, 0], shape, [int(b) for b in newBlockShape])
+    with _open(graphPath) as fi, _open(outPath) as fo:
+        gi = fi[graphBlockPrefix]
+        go = fo.require_group(graphOutPrefix)
+        go.attrs['shape'] = shape
+        keys = ('nodes', 'edges', 'edge_ids') if serializeEdges else ('nodes',)
+        for k in keys:
+            go.require_dataset(k, shape=shape, chunks=[int(b) for b in newBlockShape], dtype='uint64',
+                               compression='gzip')
+        has_ids = serializeEdges and edge_lab is not None and 'edge_ids' in gi
+
+        def read(bid):   # N5 reads in the thread pool; library calls stay on this thread
+            nb = new_blk.getBlock(int(bid))
+            old_ids = old_blk.getBlockIdsOverlappingBoundingBox(nb.begin, nb.end)
+            nodes, pairs, ids = [], [], []
+            for ob in old_ids:
+                opos = old_blk.blockGridPosition(int(ob))
+                n = gi['nodes'].read_chunk(opos)
+                if n is not None and len(n):
+                    nodes.append(node_lab[n.astype(np.int64)])
+                if serializeEdges:
+                    e = gi['edges'].read_chunk(opos)
+                    if e is not None and len(e):
+                        pairs.append(node_lab[e.reshape(-1, 2).astype(np.int64)])
+                        if has_ids:
+                            ids.append(edge_lab[gi['edge_ids'].read_chunk(opos).astype(np.int64)])
+            return new_blk.blockGridPosition(int(bid)), nodes, pairs, ids
+
+        for pos, nodes, pairs, ids in _map(read, newBlockIds, numberOfThreads):
+            if not nodes:
+                continue
+            go['nodes'].write_chunk(pos, rag.unique_labels(np.concatenate(nodes).reshape(1, 1, -1)), True)
+            if not pairs:
+                continue
+            uv = np.concatenate(pairs)
+            keep = uv[:, 0] != uv[:, 1]
+            uv = np.sort(uv[keep], axis=1)
+            if uv.shape[0] == 0:
+                continue
+            edges, _ = rag.unique_pairs(uv)
+            go['edges'].write_chunk(pos, edges.ravel(), True)
+            if has_ids:
+                out_ids = np.zeros(edges.shape[0], dtype=np.uint64)
+                out_ids[rag.map_edge_ids(edges, uv)] = np.concatenate(ids)[keep]
+                go['edge_ids'].write_chunk(pos, out_ids, True)
 
 
 def mapEdgeIds(graphPath, graphKey, subgraphKey, blockIds, numberOfThreads=1):  # noqa: N802,N803

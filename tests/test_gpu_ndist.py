@@ -159,3 +159,59 @@ def test_affinity_feature_workflow(gpu, tmp_path, offsets):
         # halo'd block, so the block path equals the whole-volume definition
         _, f_whole = O.affinity_features(lab, affs, offsets)
         check_features(feats, f_whole)
+
+
+@pytest.mark.parametrize('serialize_edges', [False, True])
+def test_serialize_merged_graph(gpu, tmp_path, serialize_edges):
+    """Next-scale sub-graphs of the blockwise multicut (multicut/reduce_problem.py:247-258):
+    nodes of every 2x block = the merged node labels of the scale-0 blocks inside it;
+    with serializeEdges the mapped, self-loop-free, unique edges and their new ids."""
+    lab, _ = S.generate(SHAPE, cell=5, seed=34, with_boundary=False)
+    p = _setup(tmp_path, lab)
+    blk, ids = _graph(p, False)
+    full = ndist.Graph(p, 'graph')
+    rng = np.random.default_rng(7)
+    n_max = int(full.maxNodeId) + 1
+    # a consecutive node labelling that merges nodes (reduce_problem.py:160-193)
+    node_lab = np.unique(rng.integers(0, n_max // 3, n_max), return_inverse=True)[1].astype(np.uint64)
+    new_uv_all = np.sort(node_lab[full.uvIds().astype(np.int64)], axis=1)
+    live = new_uv_all[:, 0] != new_uv_all[:, 1]
+    new_uv, inv = np.unique(new_uv_all[live], axis=0, return_inverse=True)
+    edge_lab = np.full(full.numberOfEdges, np.iinfo(np.uint64).max, np.uint64)
+    edge_lab[live] = inv.ravel()
+    new_bs = [2 * b for b in BLOCK]
+    nblk = blocking([0, 0, 0], list(SHAPE), new_bs)
+    new_ids = list(range(nblk.numberOfBlocks))
+    ndist.serializeMergedGraph(graphPath=p, graphBlockPrefix='s0/sub_graphs', shape=list(SHAPE),
+                               blockShape=list(BLOCK), newBlockShape=new_bs, newBlockIds=new_ids,
+                               nodeLabeling=node_lab, edgeLabeling=edge_lab, outPath=p,
+                               graphOutPrefix='s1/sub_graphs', numberOfThreads=3,
+                               serializeEdges=serialize_edges)
+    with n5.File(p, 'r') as f:
+        g = f['s1/sub_graphs']
+        assert list(g['nodes'].chunks) == new_bs
+        for b in new_ids:
+            nb = nblk.getBlock(b)
+            pos = nblk.blockGridPosition(b)
+            inner = tuple(slice(x, y) for x, y in zip(nb.begin, nb.end))
+            np.testing.assert_array_equal(g['nodes'].read_chunk(pos), np.unique(node_lab[np.unique(lab[inner])]))
+            if not serialize_edges:
+                continue
+            parts = []
+            for ob in blk.getBlockIdsOverlappingBoundingBox(nb.begin, nb.end):
+                bb = blk.getBlock(int(ob))
+                outer = tuple(slice(max(x - 1, 0), y) for x, y in zip(bb.begin, bb.end))
+                e = O.rag_edges(lab[outer])
+                if e.shape[0]:
+                    parts.append(np.sort(node_lab[e.astype(np.int64)], axis=1))
+            ref = np.concatenate(parts) if parts else np.zeros((0, 2), np.uint64)
+            ref = ref[ref[:, 0] != ref[:, 1]]
+            ref = np.unique(ref, axis=0) if ref.shape[0] else ref
+            got = g['edges'].read_chunk(pos)
+            if ref.shape[0] == 0:
+                assert got is None
+                continue
+            got = got.reshape(-1, 2)
+            np.testing.assert_array_equal(got, ref)
+            rows = np.array([np.flatnonzero((new_uv == r).all(axis=1))[0] for r in ref], dtype=np.uint64)
+            np.testing.assert_array_equal(g['edge_ids'].read_chunk(pos), rows)
