@@ -21,7 +21,8 @@ int scan_tile_rows();
 hipError_t launch_unique_tiles(const uint64_t* L, const int64_t* shape, const int64_t* b, const int64_t* e,
                                uint64_t* out, unsigned long long* count, int64_t cap, hipStream_t s);
 hipError_t launch_pack_keys(int64_t n, const uint64_t* key, int nb, uint64_t* sk, uint32_t* idx, hipStream_t s);
-hipError_t launch_pack_regions(const uint64_t* key, int64_t rcap, const RegionPrefix& pre, int nb, uint64_t* sk,
+hipError_t launch_unpack_slots(int64_t n, const uint64_t* sk, int ib, uint32_t* idx, hipStream_t s);
+hipError_t launch_pack_regions(const uint64_t* key, int64_t rcap, const RegionPrefix& pre, int nb, int ib, uint64_t* sk,
                                uint32_t* idx, hipStream_t s);
 hipError_t launch_pack_pairs(int64_t n, const uint64_t* uv, int nb, uint64_t* sk, uint32_t* idx, hipStream_t s);
 hipError_t launch_max_pairs(int64_t n, const uint64_t* uv, unsigned long long* out, hipStream_t s);
@@ -219,6 +220,13 @@ using RecordSortConfig = rocprim::default_config;
 // lose for very large ones (298 M records of configs[4]:
 // 14.1 -> 18.7 ms, the 1024-way scatter coalesces worse), so they are used up
 // to this many records (CTG_SORT_WIDE_MAX overrides).
+static bool sort_packed() {
+    static const bool v = [] {
+        const char* e = getenv("CTG_SORT_PACKED");
+        return !(e && e[0] == '0');
+    }();
+    return v;
+}
 static int64_t sort_wide_digits_max() {
     static const int64_t v = [] {
         const char* e = getenv("CTG_SORT_WIDE_MAX");
@@ -289,20 +297,36 @@ static hipError_t reduce_records(Workspace& w, const ReduceJob& J, hipStream_t s
     uint32_t* dE = w.small + 1;
     uint32_t* dN = w.small + 2;
     hipError_t e;
-    if (J.keys && J.regions) e = launch_pack_regions(J.keys, J.R.rcap, *J.regions, nb, w.sk_in, w.idx_in, s);
+    // Scan records whose slot fits beside the 2*nb key bits sort as bare u64
+    // keys (slot in the low ib bits): 16 instead of 24 bytes per record and
+    // pass, then one unpack of the slots (CTG_SORT_PACKED=0 disables).
+    const int ib = J.regions ? bits_for((uint64_t)std::max<int64_t>(J.R.cap - 1, 1)) : 0;
+    const bool packed = J.keys && J.regions && sort_packed() && 2 * nb + ib <= 64 && n <= sort_wide_digits_max();
+    if (J.keys && J.regions)
+        e = launch_pack_regions(J.keys, J.R.rcap, *J.regions, nb, packed ? ib : 0, w.sk_in, w.idx_in, s);
     else if (J.keys) e = launch_pack_keys(n, J.keys, nb, w.sk_in, w.idx_in, s);
     else e = launch_pack_pairs(n, J.pairs, nb, w.sk_in, w.idx_in, s);
     if (e != hipSuccess) return e;
     ev.mark(2);
-    if (n <= sort_wide_digits_max()) {
+    if (packed) {
+        ROCPRIM_CALL(w, rocprim::radix_sort_keys<RecordSortConfig>(t, tbytes, w.sk_in, w.sk_out, (size_t)n,
+                                                                   (unsigned)ib, (unsigned)(ib + 2 * nb), s));
+        e = launch_unpack_slots(n, w.sk_out, ib, w.idx_out, s);
+        if (e != hipSuccess) return e;
+        ev.mark(3);
+        auto key_only = rocprim::make_transform_iterator(w.sk_out, [ib] __device__(uint64_t k) { return k >> ib; });
+        ROCPRIM_CALL(w, rocprim::run_length_encode(t, tbytes, key_only, (unsigned)n, w.uniq, w.runs, dE_all, s));
+    } else if (n <= sort_wide_digits_max()) {
         ROCPRIM_CALL(w, rocprim::radix_sort_pairs<RecordSortConfig>(t, tbytes, w.sk_in, w.sk_out, w.idx_in,
                                                                     w.idx_out, (size_t)n, 0u, (unsigned)(2 * nb), s));
     } else {
         ROCPRIM_CALL(w, rocprim::radix_sort_pairs(t, tbytes, w.sk_in, w.sk_out, w.idx_in, w.idx_out, (size_t)n, 0u,
                                                   (unsigned)(2 * nb), s));
     }
-    ev.mark(3);
-    ROCPRIM_CALL(w, rocprim::run_length_encode(t, tbytes, w.sk_out, (unsigned)n, w.uniq, w.runs, dE_all, s));
+    if (!packed) {
+        ev.mark(3);
+        ROCPRIM_CALL(w, rocprim::run_length_encode(t, tbytes, w.sk_out, (unsigned)n, w.uniq, w.runs, dE_all, s));
+    }
     // offsets over the n-bound: entries past E_all are never read
     ROCPRIM_CALL(w, rocprim::exclusive_scan(t, tbytes, w.runs, w.offs, 0u, (size_t)n, rocprim::plus<uint32_t>(), s));
     ev.mark(4);

@@ -26,8 +26,10 @@ __global__ void k_pack_keys(int64_t n, const uint64_t* __restrict__ key, int nb,
 }
 
 // scan records: region r holds pre.off[r+1]-pre.off[r] keys from slot r*rcap;
-// packed densely in region order, idx = the record's slot
-__global__ void k_pack_regions(const uint64_t* __restrict__ key, int64_t rcap, RegionPrefix pre, int nb,
+// packed densely in region order, idx = the record's slot.  ib > 0: the slot
+// rides in the low ib bits of the sort key itself ((key << ib) | slot, sorted
+// on bits [ib, ib + 2nb)) and no separate index array is written.
+__global__ void k_pack_regions(const uint64_t* __restrict__ key, int64_t rcap, RegionPrefix pre, int nb, int ib,
                                uint64_t* __restrict__ sk, uint32_t* __restrict__ idx) {
     const int r = blockIdx.y;
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -35,8 +37,19 @@ __global__ void k_pack_regions(const uint64_t* __restrict__ key, int64_t rcap, R
     if (i >= pre.off[r + 1] - b) return;
     const uint64_t src = (uint64_t)r * (uint64_t)rcap + i;
     const uint64_t k = key[src];
-    sk[b + i] = ((k >> 32) << nb) | (k & 0xFFFFFFFFull);
-    idx[b + i] = (uint32_t)src;
+    const uint64_t pk = ((k >> 32) << nb) | (k & 0xFFFFFFFFull);
+    if (ib) {
+        sk[b + i] = (pk << ib) | src;
+    } else {
+        sk[b + i] = pk;
+        idx[b + i] = (uint32_t)src;
+    }
+}
+
+// packed sort keys -> record slots (the reduction's permutation)
+__global__ void k_unpack_slots(int64_t n, const uint64_t* __restrict__ sk, int ib, uint32_t* __restrict__ idx) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) idx[i] = (uint32_t)(sk[i] & ((1ull << ib) - 1ull));
 }
 
 // pack (u,v) pairs given as two u64 (merge inputs); flags labels >= 2^32
@@ -477,13 +490,19 @@ hipError_t launch_pack_keys(int64_t n, const uint64_t* key, int nb, uint64_t* sk
     hipLaunchKernelGGL(k_pack_keys, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, n, key, nb, sk, idx);
     return hipGetLastError();
 }
-hipError_t launch_pack_regions(const uint64_t* key, int64_t rcap, const RegionPrefix& pre, int nb, uint64_t* sk,
-                               uint32_t* idx, hipStream_t s) {
+hipError_t launch_pack_regions(const uint64_t* key, int64_t rcap, const RegionPrefix& pre, int nb, int ib,
+                               uint64_t* sk, uint32_t* idx, hipStream_t s) {
     uint32_t mx = 0;
     for (int r = 0; r < NREG; ++r) mx = std::max(mx, pre.off[r + 1] - pre.off[r]);
     if (mx == 0) return hipSuccess;
     if ((uint64_t)rcap * NREG > (1ull << 32)) return hipErrorInvalidValue;   // slots index as u32
-    hipLaunchKernelGGL(k_pack_regions, dim3((mx + 255) / 256, NREG), dim3(256), 0, s, key, rcap, pre, nb, sk, idx);
+    hipLaunchKernelGGL(k_pack_regions, dim3((mx + 255) / 256, NREG), dim3(256), 0, s, key, rcap, pre, nb, ib, sk,
+                       idx);
+    return hipGetLastError();
+}
+hipError_t launch_unpack_slots(int64_t n, const uint64_t* sk, int ib, uint32_t* idx, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_unpack_slots, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, n, sk, ib, idx);
     return hipGetLastError();
 }
 hipError_t launch_pack_pairs(int64_t n, const uint64_t* uv, int nb, uint64_t* sk, uint32_t* idx, hipStream_t s) {
