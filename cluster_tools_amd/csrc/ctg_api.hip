@@ -21,14 +21,14 @@ int scan_tile_rows();
 hipError_t launch_unique_tiles(const uint64_t* L, const int64_t* shape, const int64_t* b, const int64_t* e,
                                uint64_t* out, unsigned long long* count, int64_t cap, hipStream_t s);
 hipError_t launch_pack_keys(int64_t n, const uint64_t* key, int nb, uint64_t* sk, uint32_t* idx, hipStream_t s);
-hipError_t launch_unpack_slots(int64_t n, const uint64_t* sk, int ib, uint32_t* idx, hipStream_t s);
 hipError_t launch_pack_regions(const uint64_t* key, int64_t rcap, const RegionPrefix& pre, int nb, int ib, uint64_t* sk,
                                uint32_t* idx, hipStream_t s);
 hipError_t launch_pack_pairs(int64_t n, const uint64_t* uv, int nb, uint64_t* sk, uint32_t* idx, hipStream_t s);
 hipError_t launch_max_pairs(int64_t n, const uint64_t* uv, unsigned long long* out, hipStream_t s);
 hipError_t launch_reduce(int64_t E, const uint32_t* dE, const uint64_t* uniq, const uint32_t* runs,
-                         const uint32_t* offs, const uint32_t* perm, const RecordBuf& R, int wide, int stats, int nb,
-                         int need_adj, int ignore_label, double scale, double offset, const ReduceOut& O,
+                         const uint32_t* offs, const uint32_t* perm32, const uint64_t* perm64, int ib,
+                         const RecordBuf& R, int wide, int stats, int nb, int need_adj, int ignore_label, double scale,
+                         double offset, const ReduceOut& O,
                          hipStream_t s);
 hipError_t launch_compact(int64_t E, const uint32_t* dE, const uint32_t* keep, const uint32_t* pos,
                           const ReduceOut& in, const ReduceOut& out, uint32_t* dkept, hipStream_t s);
@@ -36,9 +36,8 @@ hipError_t launch_endpoints(int64_t E, const uint64_t* uniq, int nb, uint32_t* o
 hipError_t launch_u32_to_u64(int64_t n, const uint32_t* in, uint64_t* out, hipStream_t s);
 hipError_t launch_mark_nodes(int64_t E, const uint32_t* dE, const uint64_t* uniq, int nb, uint32_t* bits,
                              hipStream_t s);
-hipError_t launch_popc_words(int64_t W, const uint32_t* bits, uint32_t* cnt, hipStream_t s);
-hipError_t launch_bits_to_nodes(int64_t W, const uint32_t* bits, const uint32_t* off, uint64_t* nodes,
-                                const uint32_t* cnt, uint32_t* dN, hipStream_t s);
+hipError_t launch_bits_to_nodes(int64_t W, const uint32_t* bits, const uint32_t* off, uint64_t* nodes, uint32_t* dN,
+                                hipStream_t s);
 hipError_t launch_build_adj_set(const uint64_t* edges, int64_t E, unsigned long long* set, uint32_t mask,
                                 hipStream_t s);
 hipError_t launch_find_edges(const uint64_t* ge, int64_t n, const uint64_t* q, int64_t m, int64_t* out,
@@ -299,7 +298,7 @@ static hipError_t reduce_records(Workspace& w, const ReduceJob& J, hipStream_t s
     hipError_t e;
     // Scan records whose slot fits beside the 2*nb key bits sort as bare u64
     // keys (slot in the low ib bits): 16 instead of 24 bytes per record and
-    // pass, then one unpack of the slots (CTG_SORT_PACKED=0 disables).
+    // pass; the reduction reads the slots from the sorted keys (CTG_SORT_PACKED=0 disables).
     const int ib = J.regions ? bits_for((uint64_t)std::max<int64_t>(J.R.cap - 1, 1)) : 0;
     const bool packed = J.keys && J.regions && sort_packed() && 2 * nb + ib <= 64 && n <= sort_wide_digits_max();
     if (J.keys && J.regions)
@@ -311,8 +310,6 @@ static hipError_t reduce_records(Workspace& w, const ReduceJob& J, hipStream_t s
     if (packed) {
         ROCPRIM_CALL(w, rocprim::radix_sort_keys<RecordSortConfig>(t, tbytes, w.sk_in, w.sk_out, (size_t)n,
                                                                    (unsigned)ib, (unsigned)(ib + 2 * nb), s));
-        e = launch_unpack_slots(n, w.sk_out, ib, w.idx_out, s);
-        if (e != hipSuccess) return e;
         ev.mark(3);
         auto key_only = rocprim::make_transform_iterator(w.sk_out, [ib] __device__(uint64_t k) { return k >> ib; });
         ROCPRIM_CALL(w, rocprim::run_length_encode(t, tbytes, key_only, (unsigned)n, w.uniq, w.runs, dE_all, s));
@@ -343,8 +340,8 @@ static hipError_t reduce_records(Workspace& w, const ReduceJob& J, hipStream_t s
     }
     if (!O.edges || (J.stats && !O.feats)) return hipErrorOutOfMemory;
     O.count_out = may_drop ? nullptr : dE;   // no compaction: the kernel copies the count
-    e = launch_reduce(n, dE_all, w.uniq, w.runs, w.offs, w.idx_out, J.R, J.wide, J.stats, nb, J.need_adj,
-                      J.ignore_label, J.scale, J.offset, O, s);
+    e = launch_reduce(n, dE_all, w.uniq, w.runs, w.offs, packed ? nullptr : w.idx_out, packed ? w.sk_out : nullptr,
+                      packed ? ib : 0, J.R, J.wide, J.stats, nb, J.need_adj, J.ignore_label, J.scale, J.offset, O, s);
     if (e != hipSuccess) return e;
     if (may_drop) {
         ROCPRIM_CALL(w, rocprim::exclusive_scan(t, tbytes, w.keep, w.pos, 0u, (size_t)n, rocprim::plus<uint32_t>(), s));
@@ -372,25 +369,24 @@ static hipError_t reduce_records(Workspace& w, const ReduceJob& J, hipStream_t s
         // bitmap over [0, max label]: one pass over the sorted key table
         const int64_t W = (int64_t)(J.max_v >> 5) + 1;
         uint32_t* bits = (uint32_t*)dalloc(W * 4);
-        uint32_t* cnt = (uint32_t*)dalloc(W * 4);
         uint32_t* off = (uint32_t*)dalloc(W * 4);
         res->nodes = (uint64_t*)dalloc(std::min<int64_t>(W * 32, 2 * n) * 8);
-        if (!bits || !cnt || !off || !res->nodes) return hipErrorOutOfMemory;
+        if (!bits || !off || !res->nodes) return hipErrorOutOfMemory;
         e = hipMemsetAsync(bits, 0, W * 4, s);
         if (e != hipSuccess) return e;
         e = launch_mark_nodes(n, dE_all, w.uniq, nb, bits, s);
         if (e != hipSuccess) return e;
-        e = launch_popc_words(W, bits, cnt, s);
-        if (e != hipSuccess) return e;
-        ROCPRIM_CALL(w, rocprim::exclusive_scan(t, tbytes, cnt, off, 0u, (size_t)W, rocprim::plus<uint32_t>(), s));
-        e = launch_bits_to_nodes(W, bits, off, res->nodes, cnt, dN, s);
+        // word offsets = exclusive scan of the words' popcounts (read through the scan's input iterator)
+        auto popc = rocprim::make_transform_iterator(bits, [] __device__(uint32_t b) { return (uint32_t)__popc(b); });
+        ROCPRIM_CALL(w, rocprim::exclusive_scan(t, tbytes, popc, off, 0u, (size_t)W, rocprim::plus<uint32_t>(), s));
+        e = launch_bits_to_nodes(W, bits, off, res->nodes, dN, s);
         if (e != hipSuccess) return e;
         e = hipMemcpyAsync(w.small_host, w.small, 3 * sizeof(uint32_t), hipMemcpyDeviceToHost, s);
         if (e != hipSuccess) return e;
         e = hipStreamSynchronize(s);
         if (e != hipSuccess) return e;
         for (int i = 0; i < 3; ++i) counts[i] = w.small_host[i];
-        dfree(bits); dfree(cnt); dfree(off);
+        dfree(bits); dfree(off);
     } else {
         e = hipMemcpyAsync(w.small_host, w.small, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, s);
         if (e != hipSuccess) return e;

@@ -46,12 +46,6 @@ __global__ void k_pack_regions(const uint64_t* __restrict__ key, int64_t rcap, R
     }
 }
 
-// packed sort keys -> record slots (the reduction's permutation)
-__global__ void k_unpack_slots(int64_t n, const uint64_t* __restrict__ sk, int ib, uint32_t* __restrict__ idx) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) idx[i] = (uint32_t)(sk[i] & ((1ull << ib) - 1ull));
-}
-
 // pack (u,v) pairs given as two u64 (merge inputs); flags labels >= 2^32
 __global__ void k_pack_pairs(int64_t n, const uint64_t* __restrict__ uv, int nb, uint64_t* __restrict__ sk,
                              uint32_t* __restrict__ idx) {
@@ -186,12 +180,23 @@ __device__ __forceinline__ void load_record(const RecordBuf& R, uint32_t i, uint
     }
 }
 
+// record slot of sorted position r: a u32 index array, or the low ib bits of
+// the packed sort keys (keys-only record sort, no unpack pass)
+struct Perm {
+    const uint32_t* p32;
+    const uint64_t* p64;
+    int ib;
+    __device__ __forceinline__ uint32_t operator()(uint32_t r) const {
+        return p64 ? (uint32_t)(p64[r] & ((1ull << ib) - 1ull)) : p32[r];
+    }
+};
+
 template <bool WIDE, bool STATS>
 __global__ __launch_bounds__(256) void k_reduce_edges(int64_t E, const uint32_t* __restrict__ dE,
                                                       const uint64_t* __restrict__ uniq,
                                                       const uint32_t* __restrict__ runs,
                                                       const uint32_t* __restrict__ offs,
-                                                      const uint32_t* __restrict__ perm, RecordBuf R, int nb,
+                                                      Perm perm, RecordBuf R, int nb,
                                                       int need_adj, int ignore_label, double scale, double offset,
                                                       ReduceOut O) {
     const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -206,7 +211,7 @@ __global__ __launch_bounds__(256) void k_reduce_edges(int64_t E, const uint32_t*
         if (need_adj) {
             const uint32_t b = offs[e], n = runs[e];
             for (uint32_t r = b; r < b + n; ++r) {
-                const uint32_t i = perm[r];
+                const uint32_t i = perm(r);
                 flags |= R.hist[(size_t)i * (WIDE ? WREC_WORDS : NREC_STRIDE) + (WIDE ? 42 : NREC_OFF + 21)] & ADJ_FLAG;
             }
         } else {
@@ -222,7 +227,7 @@ __global__ __launch_bounds__(256) void k_reduce_edges(int64_t E, const uint32_t*
         double sum = 0.0, sq = 0.0;
         const uint32_t b = offs[e], n = runs[e];
         for (uint32_t r = b; r < b + n; ++r) {
-            const uint32_t i = perm[r];
+            const uint32_t i = perm(r);
             load_record<WIDE>(R, i, h, cnt, flags, mn, mx, sum, sq);
         }
         // need_adj: 0 every record is an edge (boundary maps), 1 keep edges seen
@@ -306,19 +311,13 @@ __global__ void k_mark_nodes(int64_t E, const uint32_t* __restrict__ dE, const u
     atomicOr(&bits[v >> 5], 1u << (v & 31));
 }
 
-__global__ void k_popc_words(int64_t W, const uint32_t* __restrict__ bits, uint32_t* __restrict__ cnt) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < W) cnt[i] = __popc(bits[i]);
-}
-
 __global__ void k_bits_to_nodes(int64_t W, const uint32_t* __restrict__ bits, const uint32_t* __restrict__ off,
-                                uint64_t* __restrict__ nodes, const uint32_t* __restrict__ cnt,
-                                uint32_t* __restrict__ dN) {
+                                uint64_t* __restrict__ nodes, uint32_t* __restrict__ dN) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i == W - 1) *dN = off[i] + cnt[i];   // node count
     if (i >= W) return;
     uint32_t b = bits[i];
     uint32_t o = off[i];
+    if (i == W - 1) *dN = o + __popc(b);   // node count
     while (b) {
         const int k = __ffs(b) - 1;
         nodes[o++] = (uint64_t)(i * 32 + k);
@@ -388,14 +387,9 @@ hipError_t launch_mark_nodes(int64_t E, const uint32_t* dE, const uint64_t* uniq
                            E, dE, uniq, nb, bits);
     return hipGetLastError();
 }
-hipError_t launch_popc_words(int64_t W, const uint32_t* bits, uint32_t* cnt, hipStream_t s) {
-    hipLaunchKernelGGL(k_popc_words, dim3((unsigned)((W + 255) / 256)), dim3(256), 0, s, W, bits, cnt);
-    return hipGetLastError();
-}
-hipError_t launch_bits_to_nodes(int64_t W, const uint32_t* bits, const uint32_t* off, uint64_t* nodes,
-                                const uint32_t* cnt, uint32_t* dN, hipStream_t s) {
-    hipLaunchKernelGGL(k_bits_to_nodes, dim3((unsigned)((W + 255) / 256)), dim3(256), 0, s, W, bits, off, nodes, cnt,
-                       dN);
+hipError_t launch_bits_to_nodes(int64_t W, const uint32_t* bits, const uint32_t* off, uint64_t* nodes, uint32_t* dN,
+                                hipStream_t s) {
+    hipLaunchKernelGGL(k_bits_to_nodes, dim3((unsigned)((W + 255) / 256)), dim3(256), 0, s, W, bits, off, nodes, dN);
     return hipGetLastError();
 }
 
@@ -500,11 +494,6 @@ hipError_t launch_pack_regions(const uint64_t* key, int64_t rcap, const RegionPr
                        idx);
     return hipGetLastError();
 }
-hipError_t launch_unpack_slots(int64_t n, const uint64_t* sk, int ib, uint32_t* idx, hipStream_t s) {
-    if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_unpack_slots, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, n, sk, ib, idx);
-    return hipGetLastError();
-}
 hipError_t launch_pack_pairs(int64_t n, const uint64_t* uv, int nb, uint64_t* sk, uint32_t* idx, hipStream_t s) {
     if (n == 0) return hipSuccess;
     hipLaunchKernelGGL(k_pack_pairs, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, n, uv, nb, sk, idx);
@@ -516,10 +505,11 @@ hipError_t launch_max_pairs(int64_t n, const uint64_t* uv, unsigned long long* o
     return hipGetLastError();
 }
 hipError_t launch_reduce(int64_t E, const uint32_t* dE, const uint64_t* uniq, const uint32_t* runs,
-                         const uint32_t* offs, const uint32_t* perm, const RecordBuf& R, int wide, int stats, int nb,
-                         int need_adj, int ignore_label, double scale, double offset, const ReduceOut& O,
-                         hipStream_t s) {
+                         const uint32_t* offs, const uint32_t* perm32, const uint64_t* perm64, int ib,
+                         const RecordBuf& R, int wide, int stats, int nb, int need_adj, int ignore_label, double scale,
+                         double offset, const ReduceOut& O, hipStream_t s) {
     if (E == 0) return hipSuccess;
+    const Perm perm{perm32, perm64, ib};
     dim3 g((unsigned)((E + 255) / 256)), b(256);
     if (wide) {
         if (stats) hipLaunchKernelGGL((k_reduce_edges<true, true>), g, b, 0, s, E, dE, uniq, runs, offs, perm, R, nb, need_adj, ignore_label, scale, offset, O);
