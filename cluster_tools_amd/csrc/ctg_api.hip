@@ -340,6 +340,10 @@ static hipError_t reduce_records(Workspace& w, const ReduceJob& J, hipStream_t s
     }
     if (!O.edges || (J.stats && !O.feats)) return hipErrorOutOfMemory;
     O.count_out = may_drop ? nullptr : dE;   // no compaction: the kernel copies the count
+    {
+        static const int ablate = [] { const char* v = getenv("CTG_REDUCE_ABLATE"); return v ? atoi(v) : 0; }();
+        O.ablate = ablate;
+    }
     e = launch_reduce(n, dE_all, w.uniq, w.runs, w.offs, packed ? nullptr : w.idx_out, packed ? w.sk_out : nullptr,
                       packed ? ib : 0, J.R, J.wide, J.stats, nb, J.need_adj, J.ignore_label, J.scale, J.offset, O, s);
     if (e != hipSuccess) return e;

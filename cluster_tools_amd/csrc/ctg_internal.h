@@ -130,6 +130,7 @@ struct ReduceOut {
     uint32_t* wstats;     // WREC_WORDS*E or null
     double2* wsums;       // E or null
     uint32_t* count_out;  // null, or receives the edge count (no compaction follows)
+    int ablate;           // diagnostics (CTG_REDUCE_ABLATE): 1 no quantiles, 2 no record loads, 4 no feature stores
 };
 
 struct Workspace {

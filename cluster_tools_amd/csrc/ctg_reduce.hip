@@ -77,7 +77,7 @@ __global__ void k_max_pairs(int64_t n, const uint64_t* __restrict__ uv, unsigned
 // interior quantile q (0.1 .. 0.9) is interpolated on the first segment with
 // cum(a) < q*count <= cum(b) and written straight to out[q] (global memory:
 // no dynamically indexed register arrays, no scratch).
-__device__ __forceinline__ double qv5(int i) {
+__host__ __device__ __forceinline__ double qv5(int i) {
     return i == 0 ? 0.1 : i == 1 ? 0.25 : i == 2 ? 0.5 : i == 3 ? 0.75 : 0.9;
 }
 
@@ -85,7 +85,7 @@ __device__ __forceinline__ double qv5(int i) {
 // (the bin walk is fully unrolled, so the array is never indexed dynamically
 // and stays in registers - no LDS copy, no scratch)
 template <typename HL>
-__device__ __forceinline__ void vigra_quantiles(const HL& hl, double count, double vmin, double vmax, double scale,
+__host__ __device__ __forceinline__ void vigra_quantiles(const HL& hl, double count, double vmin, double vmax, double scale,
                                                 double offset, double* __restrict__ out) {
     const double inv = 1.0 / scale;
     int q = 0;
@@ -133,6 +133,74 @@ __device__ __forceinline__ void vigra_quantiles(const HL& hl, double count, doub
         consume(kp_pend, ch_pend);
     } else {
         consume(scale * (vmax - offset), count);  // replaces the last keypoint
+    }
+}
+
+// The same quantiles without walking the keypoint list: the keypoints' counts
+// are 0, left, then per non-empty bin k (cum before k, a duplicate point at
+// x = k) and (cum after k, at x = k + 1), then for right outliers
+// (cum, at x = 40) and (count, at x = mapped max); the last point is replaced
+// by (mapped max, count) when there are no right outliers.  Quantile q
+// interpolates on the segment ending at the first keypoint whose count
+// reaches q*count, so one integer pass over the 40 bins finds, per q, the
+// crossing bin and the counts on both sides (count >= q*count <=> count >=
+// ceil(q*count) for integer counts), and the f64 arithmetic runs only at the
+// five crossings.  Same segment endpoints and the same interpolation formula
+// as vigra_quantiles, hence the same bits (tools/quantile_fuzz.hip).
+template <typename HL>
+__host__ __device__ __forceinline__ void vigra_quantiles_cross(const HL& hl, double count, double vmin, double vmax,
+                                                               double scale, double offset,
+                                                               double* __restrict__ out) {
+    const double inv = 1.0 / scale;
+    const double p0 = scale * (vmin - offset), pe = scale * (vmax - offset);
+    const uint32_t left = hl[0], right = hl[NSLOTS - 1];
+    uint32_t T[5], kq[5], cb[5], ca[5];
+#pragma unroll
+    for (int q = 0; q < 5; ++q) {
+        T[q] = (uint32_t)ceil(count * qv5(q));
+        kq[q] = 0;
+        cb[q] = left;
+        ca[q] = 0xFFFFFFFFu;
+    }
+    uint32_t cum = left;
+#pragma unroll
+    for (int k = 0; k < NBINS; ++k) {
+        const uint32_t nc = cum + (uint32_t)hl[k + 1];
+#pragma unroll
+        for (int q = 0; q < 5; ++q) {
+            const bool below = nc < T[q];
+            cb[q] = below ? nc : cb[q];
+            kq[q] = below ? (uint32_t)(k + 1) : kq[q];
+            ca[q] = (!below && nc < ca[q]) ? nc : ca[q];
+        }
+        cum = nc;
+    }
+    // cum = left + every bin = count - right
+#pragma unroll
+    for (int q = 0; q < 5; ++q) {
+        const double qc = count * qv5(q);
+        double pkp, pch, kp, ch;
+        if (left >= T[q]) {                 // segment P0 -> (0, left)
+            pkp = p0;
+            pch = 0.0;
+            const bool last = cum == left && right == 0;
+            kp = last ? pe : 0.0;
+            ch = last ? count : (double)left;
+        } else if (kq[q] < (uint32_t)NBINS) {   // inside bin kq
+            const bool first = cb[q] == left;   // no non-empty bin before kq
+            pkp = (first && left == 0 && !(p0 <= (double)kq[q])) ? p0 : (double)kq[q];
+            pch = (double)cb[q];
+            const bool last = ca[q] == cum && right == 0;
+            kp = last ? pe : (double)(kq[q] + 1);
+            ch = last ? count : (double)ca[q];
+        } else {                            // right-outlier segment (40, count - right) -> (mapped max, count)
+            pkp = (double)NBINS;
+            pch = (double)cum;
+            kp = pe;
+            ch = count;
+        }
+        const double t = (qc - pch) / (ch - pch) * (kp - pkp);
+        out[q] = inv * (t + pkp) + offset;
     }
 }
 
@@ -226,9 +294,16 @@ __global__ __launch_bounds__(256) void k_reduce_edges(int64_t E, const uint32_t*
         uint32_t cnt = 0, mn = ORD_POS_INF, mx = ORD_NEG_INF;
         double sum = 0.0, sq = 0.0;
         const uint32_t b = offs[e], n = runs[e];
-        for (uint32_t r = b; r < b + n; ++r) {
-            const uint32_t i = perm(r);
-            load_record<WIDE>(R, i, h, cnt, flags, mn, mx, sum, sq);
+        if (O.ablate & 2) {
+            cnt = n;
+            h[1] = n;
+            mn = mx = 0x3F800000u ^ 0x80000000u;
+            sum = sq = (double)n;
+        } else {
+            for (uint32_t r = b; r < b + n; ++r) {
+                const uint32_t i = perm(r);
+                load_record<WIDE>(R, i, h, cnt, flags, mn, mx, sum, sq);
+            }
         }
         // need_adj: 0 every record is an edge (boundary maps), 1 keep edges seen
         // on a nearest-neighbour face, 2 keep all and carry the flag (partials)
@@ -250,6 +325,13 @@ __global__ __launch_bounds__(256) void k_reduce_edges(int64_t E, const uint32_t*
         }
         if (!O.feats) return;
         double* o = O.feats + (size_t)e * N_FEATURES;
+        if (O.ablate & 4) {   // keep the values live without the 80-B row stores
+            double t = sum + sq + (double)cnt + (double)mn + (double)mx;
+#pragma unroll
+            for (int j = 0; j < NSLOTS; ++j) t += (double)h[j];
+            if (t == -1.0) o[0] = t;
+            return;
+        }
         if (cnt == 0) {
 #pragma unroll
             for (int j = 0; j < N_FEATURES; ++j) o[j] = 0.0;
@@ -264,7 +346,7 @@ __global__ __launch_bounds__(256) void k_reduce_edges(int64_t E, const uint32_t*
         o[1] = var;
         o[2] = vmin;
         o[3] = o[4] = o[5] = o[6] = o[7] = 0.0;
-        vigra_quantiles(h, c, vmin, vmax, scale, offset, o + 3);
+        if (!(O.ablate & 1)) vigra_quantiles_cross(h, c, vmin, vmax, scale, offset, o + 3);
         o[8] = vmax;
         o[9] = c;
     }

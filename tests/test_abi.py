@@ -68,3 +68,22 @@ def test_product_package_does_not_import_oracle():
                 with open(os.path.join(dirpath, f)) as fh:
                     src = fh.read()
                 assert not re.search(r'^\s*(from|import)\s+oracle\b', src, re.M), f
+
+
+def test_quantile_crossing_matches_keypoint_walk(tmp_path):
+    """The reduction's quantiles (vigra_quantiles_cross: crossing search over the
+    bins) are bit-identical to the keypoint walk restating vigra's
+    computeStandardQuantiles, on 2 M random histograms incl. outliers, bin-edge
+    minima/maxima and single-bin edges (host build of the same device code)."""
+    import shutil
+    import subprocess
+    hipcc = shutil.which('hipcc') or '/opt/rocm/bin/hipcc'
+    if not os.path.exists(hipcc):
+        pytest.skip('hipcc not available')
+    exe = str(tmp_path / 'qfuzz')
+    src = os.path.join(ROOT, 'tools', 'quantile_fuzz.hip')
+    subprocess.run([hipcc, '-O2', '-std=c++17', '--offload-arch=gfx950', src, '-o', exe], check=True,
+                   capture_output=True, timeout=300)
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-2000:]
+    assert ' 0 / ' in r.stdout or r.stdout.startswith('0 / ')
