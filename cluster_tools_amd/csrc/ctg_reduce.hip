@@ -342,13 +342,15 @@ __global__ __launch_bounds__(256) void k_reduce_edges(int64_t E, const uint32_t*
         double var = (sq - sum * mean) / c;
         if (var < 0.0) var = 0.0;
         const double vmin = (double)ord2f(mn), vmax = (double)ord2f(mx);
-        o[0] = mean;
-        o[1] = var;
-        o[2] = vmin;
-        o[3] = o[4] = o[5] = o[6] = o[7] = 0.0;
-        if (!(O.ablate & 1)) vigra_quantiles_cross(h, c, vmin, vmax, scale, offset, o + 3);
-        o[8] = vmax;
-        o[9] = c;
+        double qv[5] = {0.0, 0.0, 0.0, 0.0, 0.0};   // registers (constant indices after unrolling)
+        if (!(O.ablate & 1)) vigra_quantiles_cross(h, c, vmin, vmax, scale, offset, qv);
+        // the 80-B row as five 16-B stores (rows are 16-B aligned)
+        double2* o2 = reinterpret_cast<double2*>(o);
+        o2[0] = make_double2(mean, var);
+        o2[1] = make_double2(vmin, qv[0]);
+        o2[2] = make_double2(qv[1], qv[2]);
+        o2[3] = make_double2(qv[3], qv[4]);
+        o2[4] = make_double2(vmax, c);
     }
 }
 
