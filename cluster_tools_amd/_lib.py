@@ -48,6 +48,8 @@ PROTOTYPES = {
     'ctg_unique_labels': (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, ctypes.c_int, c_vp, ctypes.POINTER(c_vp)]),
     'ctg_merge_stats': (ctypes.c_int, [c_vp, c_vp, c_vp, ctypes.c_int64, ctypes.c_double, ctypes.c_double,
                                        ctypes.c_int, ctypes.c_int, c_vp, ctypes.POINTER(c_vp)]),
+    'ctg_merge_feature_rows': (ctypes.c_int, [c_vp, c_vp, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, c_vp,
+                                              ctypes.c_int, c_vp]),
     'ctg_unique_pairs': (ctypes.c_int, [c_vp, ctypes.c_int64, ctypes.c_int, c_vp, ctypes.POINTER(c_vp)]),
     'ctg_unique_values': (ctypes.c_int, [c_vp, ctypes.c_int64, ctypes.c_int, c_vp, ctypes.POINTER(c_vp)]),
     'ctg_map_edge_ids': (ctypes.c_int, [c_vp, ctypes.c_int64, c_vp, ctypes.c_int64, c_vp, ctypes.c_int, c_vp]),
@@ -64,6 +66,7 @@ PROTOTYPES = {
     'ctg_synth_volume': (ctypes.c_int, [c_vp, c_vp, c_vp, ctypes.c_int64, c_vp, ctypes.c_int, ctypes.c_uint64,
                                         ctypes.c_uint64, ctypes.c_double, c_vp]),
     'ctg_synth_affinities': (ctypes.c_int, [c_vp, c_vp, c_vp, ctypes.c_int, c_vp, c_vp]),
+    'ctg_trim': (ctypes.c_int, []),
     'ctg_set_profiling': (ctypes.c_int, [ctypes.c_int]),
     'ctg_last_timings': (ctypes.c_int, [c_dblp, ctypes.c_int]),
 }

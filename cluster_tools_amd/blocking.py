@@ -103,11 +103,26 @@ class blocking:  # noqa: N801  (nifty's spelling)
         return np.array(keep, dtype=np.uint64)
 
 
-def blocks_in_volume(shape, block_shape, roi_begin=None, roi_end=None):
-    """vu.blocks_in_volume without the block_list_path option
-    (utils/volume_utils.py:31-73)."""
+def blocks_in_volume(shape, block_shape, roi_begin=None, roi_end=None, block_list_path=None,
+                     return_blocking=False):
+    """vu.blocks_in_volume (utils/volume_utils.py:31-73): all block ids, those
+    overlapping an ROI, those listed in a JSON file, or the intersection."""
+    import json
+    import os
+    assert len(shape) == len(block_shape)
+    assert (roi_begin is None) == (roi_end is None)
+    if block_list_path is not None and not os.path.exists(block_list_path):
+        raise AssertionError("Was given block_list_path %s that doesn't exist" % block_list_path)
     b = blocking([0] * len(shape), list(shape), list(block_shape))
-    if roi_begin is None:
-        return list(range(b.numberOfBlocks))
-    roi_end = [s if e is None else e for e, s in zip(roi_end, shape)]
-    return b.getBlockIdsOverlappingBoundingBox(list(roi_begin), list(roi_end)).tolist()
+    if roi_begin is None and block_list_path is None:
+        ids = list(range(b.numberOfBlocks))
+    else:
+        ids = None
+        if roi_begin is not None:
+            roi_end = [s if e is None else e for e, s in zip(roi_end, shape)]
+            ids = b.getBlockIdsOverlappingBoundingBox(list(roi_begin), list(roi_end)).tolist()
+        if block_list_path is not None:
+            with open(block_list_path) as f:
+                listed = json.load(f)
+            ids = listed if ids is None else np.intersect1d(listed, ids).tolist()
+    return (ids, b) if return_blocking else ids

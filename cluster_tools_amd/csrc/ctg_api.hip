@@ -52,6 +52,10 @@ hipError_t launch_remap_dense64(const uint64_t* L, int64_t V, const uint64_t* U,
                                 hipStream_t s);
 hipError_t launch_synth_aff(const float* b, float* out, const int64_t* shape, int n_channels, const int32_t* off,
                             hipStream_t s);
+hipError_t launch_row_keys(int64_t n, const uint64_t* ids, uint64_t begin, uint64_t end, uint32_t* key,
+                           uint32_t* idx, uint32_t* bad, hipStream_t s);
+hipError_t launch_merge_feature_rows(int64_t n, const uint32_t* key, const uint32_t* idx, const double* rows,
+                                     double* out, hipStream_t s);
 
 static thread_local std::string g_err;
 void set_error(const std::string& msg) { g_err = msg; }
@@ -463,6 +467,36 @@ int ctg_init(int device) {
     }
     CTG_CHECK(hipSetDevice(device));
     CTG_CHECK(ws_init(ws(device)));
+    return CTG_OK;
+}
+
+int ctg_trim(void) {
+    // hand every cached device block of the current device back to HIP: the
+    // workspace (records, sort scratch, staging) and the allocator's pool
+    const int d = cur_dev();
+    Workspace& w = ws(d);
+    CTG_CHECK(hipDeviceSynchronize());
+    dfree(w.rec.key); dfree(w.rec.sums); dfree(w.rec.hist);
+    w.rec = RecordBuf{};
+    dfree(w.sk_in); dfree(w.sk_out); dfree(w.idx_in); dfree(w.idx_out);
+    dfree(w.uniq); dfree(w.runs); dfree(w.offs); dfree(w.keep); dfree(w.pos);
+    w.sk_in = w.sk_out = w.uniq = nullptr;
+    w.idx_in = w.idx_out = w.runs = w.offs = w.keep = w.pos = nullptr;
+    w.sort_cap = 0;
+    dfree(w.temp);
+    w.temp = nullptr;
+    w.temp_bytes = 0;
+    for (int i = 0; i < 2; ++i) {
+        dfree(w.stage[i]);
+        w.stage[i] = nullptr;
+        w.stage_bytes[i] = 0;
+    }
+    std::lock_guard<std::mutex> g(g_mu);
+    for (auto& kv : g_pool[d & 63]) {
+        g_sizes.erase(kv.second);
+        CTG_CHECK(hipFree(kv.second));
+    }
+    g_pool[d & 63].clear();
     return CTG_OK;
 }
 
@@ -1030,6 +1064,75 @@ int ctg_merge_stats(const uint64_t* keys, const double* sums, const uint32_t* re
         return CTG_ERR_HIP;
     }
     *out = r;
+    return CTG_OK;
+}
+
+int ctg_merge_feature_rows(const uint64_t* ids, const double* rows, int64_t n, int64_t id_begin, int64_t id_end,
+                           double* out, int mem, void* stream) {
+    if (n < 0 || id_end < id_begin || (n > 0 && (!ids || !rows)) || (id_end > id_begin && !out)) {
+        set_error("ctg_merge_feature_rows: bad arguments");
+        return CTG_ERR_ARG;
+    }
+    if (id_end - id_begin > 0xFFFFFFFFll || n > 0xFFFFFFFFll) {
+        set_error("ctg_merge_feature_rows: more than 2^32 edges or rows in one call");
+        return CTG_ERR_UNSUPPORTED;
+    }
+    const int64_t E = id_end - id_begin;
+    if (E == 0) return CTG_OK;
+    const int dev = cur_dev();
+    Workspace& w = ws(dev);
+    CTG_CHECK(ws_init(w));
+    hipStream_t s = (hipStream_t)stream;
+    const bool host = mem == CTG_MEM_HOST;
+    const uint64_t* di = ids;
+    const double* dr = rows;
+    double* dout = out;
+    void* owned[3] = {nullptr, nullptr, nullptr};
+    if (host) {
+        owned[0] = dalloc(std::max<int64_t>(n, 1) * 8);
+        owned[1] = dalloc(std::max<int64_t>(n, 1) * N_FEATURES * 8);
+        owned[2] = dalloc(E * N_FEATURES * 8);
+        if (!owned[0] || !owned[1] || !owned[2]) {
+            set_error("ctg_merge_feature_rows: out of device memory");
+            return CTG_ERR_NOMEM;
+        }
+        if (n) {
+            CTG_CHECK(hipMemcpyAsync(owned[0], ids, n * 8, hipMemcpyHostToDevice, s));
+            CTG_CHECK(hipMemcpyAsync(owned[1], rows, n * N_FEATURES * 8, hipMemcpyHostToDevice, s));
+        }
+        di = (const uint64_t*)owned[0];
+        dr = (const double*)owned[1];
+        dout = (double*)owned[2];
+    }
+    CTG_CHECK(hipMemsetAsync(dout, 0, E * N_FEATURES * 8, s));
+    if (n) {
+        uint32_t* k_in = (uint32_t*)dalloc(n * 4);
+        uint32_t* k_out = (uint32_t*)dalloc(n * 4);
+        uint32_t* i_in = (uint32_t*)dalloc(n * 4);
+        uint32_t* i_out = (uint32_t*)dalloc(n * 4);
+        if (!k_in || !k_out || !i_in || !i_out) {
+            set_error("ctg_merge_feature_rows: out of device memory");
+            return CTG_ERR_NOMEM;
+        }
+        CTG_CHECK(hipMemsetAsync(w.small + 3, 0, 4, s));
+        CTG_CHECK(launch_row_keys(n, di, (uint64_t)id_begin, (uint64_t)id_end, k_in, i_in, w.small + 3, s));
+        const unsigned kb = (unsigned)bits_for((uint64_t)std::max<int64_t>(E - 1, 1));
+        size_t tb = 0;
+        CTG_CHECK(rocprim::radix_sort_pairs(nullptr, tb, k_in, k_out, i_in, i_out, (size_t)n, 0u, kb, s));
+        ensure(&w.temp, w.temp_bytes, tb + 256);
+        tb = w.temp_bytes;
+        CTG_CHECK(rocprim::radix_sort_pairs(w.temp, tb, k_in, k_out, i_in, i_out, (size_t)n, 0u, kb, s));
+        CTG_CHECK(launch_merge_feature_rows(n, k_out, i_out, dr, dout, s));
+        CTG_CHECK(hipMemcpyAsync(w.small_host + 3, w.small + 3, 4, hipMemcpyDeviceToHost, s));
+        dfree(k_in); dfree(k_out); dfree(i_in); dfree(i_out);
+    }
+    if (host) CTG_CHECK(hipMemcpyAsync(out, dout, E * N_FEATURES * 8, hipMemcpyDeviceToHost, s));
+    CTG_CHECK(hipStreamSynchronize(s));
+    for (void* p : owned) dfree(p);
+    if (n && w.small_host[3]) {
+        set_error("ctg_merge_feature_rows: an edge id lies outside [id_begin, id_end)");
+        return CTG_ERR_ARG;
+    }
     return CTG_OK;
 }
 

@@ -563,6 +563,90 @@ hipError_t launch_gather_labels(const uint64_t* U, uint64_t* x, int64_t n, hipSt
     return hipGetLastError();
 }
 
+// Reference-layout feature rows (10 float64 columns, no histograms) of the
+// same edge from several blocks -> one row (mergeFeatureBlocks without the
+// statistics companion, features/merge_edge_features.py:141-147).  The rows
+// are sorted by edge (key = id - begin); the head of every run combines its
+// rows in sorted order: count sum, count-weighted mean, exact pooled variance
+// sum(c * (var + (mean_i - mean)^2)) / N, min / max over non-empty rows and
+// count-weighted quantiles.
+__global__ void k_merge_feature_rows(int64_t n, const uint32_t* __restrict__ key, const uint32_t* __restrict__ idx,
+                                     const double* __restrict__ rows, double* __restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t k = key[i];
+    if (i > 0 && key[i - 1] == k) return;
+    int64_t j1 = i;
+    while (j1 < n && key[j1] == k) ++j1;
+    double N = 0.0, S = 0.0, q[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
+    double mn = INFINITY, mx = -INFINITY;
+    int n_rows = 0;
+    const double* only = nullptr;
+    for (int64_t j = i; j < j1; ++j) {
+        const double* r = rows + (size_t)idx[j] * N_FEATURES;
+        const double c = r[9];
+        if (!(c > 0.0)) continue;
+        ++n_rows;
+        only = r;
+        N += c;
+        S += c * r[0];
+        mn = fmin(mn, r[2]);
+        mx = fmax(mx, r[8]);
+#pragma unroll
+        for (int t = 0; t < 5; ++t) q[t] += c * r[3 + t];
+    }
+    double* o = out + (size_t)k * N_FEATURES;
+    if (N == 0.0) return;   // rows stay zero (pre-filled)
+    if (n_rows == 1) {      // one non-empty block: its row is the edge's row, bit for bit
+        for (int t = 0; t < N_FEATURES; ++t) o[t] = only[t];
+        return;
+    }
+    const double mean = S / N;
+    double M2 = 0.0;
+    for (int64_t j = i; j < j1; ++j) {
+        const double* r = rows + (size_t)idx[j] * N_FEATURES;
+        const double c = r[9];
+        if (!(c > 0.0)) continue;
+        const double d = r[0] - mean;
+        M2 += c * (r[1] + d * d);
+    }
+    o[0] = mean;
+    o[1] = M2 / N;
+    o[2] = mn;
+#pragma unroll
+    for (int t = 0; t < 5; ++t) o[3 + t] = q[t] / N;
+    o[8] = mx;
+    o[9] = N;
+}
+
+// ids outside [begin, end) raise *bad (the host reports them)
+__global__ void k_row_keys(int64_t n, const uint64_t* __restrict__ ids, uint64_t begin, uint64_t end,
+                           uint32_t* __restrict__ key, uint32_t* __restrict__ idx, uint32_t* __restrict__ bad) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t id = ids[i];
+    const bool ok = id >= begin && id < end;
+    if (!ok) atomicOr(bad, 1u);
+    key[i] = ok ? (uint32_t)(id - begin) : 0u;
+    idx[i] = (uint32_t)i;
+}
+
+hipError_t launch_row_keys(int64_t n, const uint64_t* ids, uint64_t begin, uint64_t end, uint32_t* key,
+                           uint32_t* idx, uint32_t* bad, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_row_keys, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, n, ids, begin, end, key, idx,
+                       bad);
+    return hipGetLastError();
+}
+
+hipError_t launch_merge_feature_rows(int64_t n, const uint32_t* key, const uint32_t* idx, const double* rows,
+                                     double* out, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_merge_feature_rows, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, n, key, idx, rows,
+                       out);
+    return hipGetLastError();
+}
+
 hipError_t launch_pack_keys(int64_t n, const uint64_t* key, int nb, uint64_t* sk, uint32_t* idx, hipStream_t s) {
     if (n == 0) return hipSuccess;
     hipLaunchKernelGGL(k_pack_keys, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, n, key, nb, sk, idx);

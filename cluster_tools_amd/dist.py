@@ -84,42 +84,67 @@ def unpack_rows(rows):
     return keys, sums, recs
 
 
-def weighted_splitters(samples, counts, world):
-    """Range splitters (world-1 values) from per-rank samples of sorted keys.
+SIGN = -(1 << 63)         # xor with this maps uint64 order onto int64 order
 
-    samples: (world, S) int64, row r an evenly spaced sample of rank r's sorted
-    keys (meaningless where counts[r] == 0); counts: (world,) key totals.  Each
-    sample of rank r stands for counts[r]/S keys.  Deterministic, so every
-    rank computes the same splitters from the same gathered data.
+
+def _ordered(k):
+    """int64 view of uint64 labels -> int64 values in the same (unsigned) order."""
+    return torch.bitwise_xor(k, SIGN)
+
+
+def weighted_splitters_t(samples, counts, world):
+    """Range splitters (world-1 values, torch) from per-rank samples of sorted keys.
+
+    samples: (world, S) int64 tensor, row r an evenly spaced sample of rank r's
+    sorted keys (meaningless where counts[r] == 0); counts: (world,) key
+    totals.  Each sample of rank r stands for counts[r]/S keys.  Pure tensor
+    arithmetic on the tensors' device (no host round trip), deterministic, so
+    every rank computes the same splitters from the same gathered data.
     """
-    samples = np.asarray(samples, dtype=np.int64)
-    counts = np.asarray(counts, dtype=np.float64)
     S = samples.shape[1]
-    w = np.repeat(counts / S, S)
+    dev = samples.device
+    w = (counts.to(torch.float64) / S).repeat_interleave(S)
     v = samples.reshape(-1)
     keep = w > 0
-    v, w = v[keep], w[keep]
-    if v.size == 0:
-        return np.zeros(world - 1, dtype=np.int64)
-    order = np.argsort(v, kind='stable')
+    # dropped entries become +inf-weight-free sentinels at the end of the order
+    v = torch.where(keep, v, torch.full_like(v, torch.iinfo(torch.int64).max))
+    w = torch.where(keep, w, torch.zeros_like(w))
+    order = torch.sort(v, stable=True).indices
     v, w = v[order], w[order]
-    cw = np.cumsum(w)
+    cw = torch.cumsum(w, 0)
     total = cw[-1]
-    targets = total * np.arange(1, world) / world
-    idx = np.minimum(np.searchsorted(cw, targets, side='left'), v.size - 1)
-    return v[idx].astype(np.int64)
+    targets = total * torch.arange(1, world, device=dev, dtype=torch.float64) / world
+    n_keep = keep.sum()
+    idx = torch.searchsorted(cw, targets, side='left')
+    idx = torch.minimum(idx, torch.clamp(n_keep - 1, min=0))
+    out = v[idx]
+    return torch.where(n_keep > 0, out, torch.zeros_like(out))
+
+
+def weighted_splitters(samples, counts, world):
+    """numpy front end of weighted_splitters_t (tests, host callers)."""
+    t = weighted_splitters_t(torch.as_tensor(np.asarray(samples, dtype=np.int64)),
+                             torch.as_tensor(np.asarray(counts, dtype=np.float64)), world)
+    return t.numpy().astype(np.int64)
+
+
+def split_counts_t(sorted_keys, splitters):
+    """Rows per destination rank (tensor, on the keys' device) for a key column
+    sorted ascending: rank k gets splitters[k-1] <= key < splitters[k]."""
+    n = sorted_keys.shape[0]
+    dev = sorted_keys.device
+    if splitters.numel() == 0:
+        return torch.tensor([n], dtype=torch.int64, device=dev)
+    pos = torch.searchsorted(sorted_keys.contiguous(), splitters.to(dev), right=False)
+    bounds = torch.cat([torch.zeros(1, dtype=torch.int64, device=dev), pos,
+                        torch.full((1,), n, dtype=torch.int64, device=dev)])
+    return bounds[1:] - bounds[:-1]
 
 
 def split_counts(sorted_keys, splitters):
-    """Rows per destination rank for a key column sorted ascending:
-    rank k gets splitters[k-1] <= key < splitters[k]."""
-    n = sorted_keys.shape[0]
-    if len(splitters) == 0:
-        return [n]
-    sp = torch.as_tensor(np.asarray(splitters), dtype=torch.int64, device=sorted_keys.device)
-    pos = torch.searchsorted(sorted_keys.contiguous(), sp, right=False).cpu().tolist()
-    bounds = [0] + pos + [n]
-    return [bounds[i + 1] - bounds[i] for i in range(len(bounds) - 1)]
+    """List front end of split_counts_t."""
+    sp = torch.as_tensor(np.asarray(splitters, dtype=np.int64))
+    return split_counts_t(sorted_keys, sp).cpu().tolist()
 
 
 def _wire_device(device, group):
@@ -129,19 +154,22 @@ def _wire_device(device, group):
     return torch.device('cpu') if dist.get_backend(group) == 'gloo' else device
 
 
-def exchange(rows, send_counts, group=None):
-    """all_to_all of variable-length row blocks; returns the received rows."""
+def exchange(rows, send_counts, group=None, recv_counts=None):
+    """all_to_all of variable-length row blocks; returns the received rows.
+    With ``recv_counts`` (known from an earlier all_gather of the count
+    matrix) no count exchange and no host round trip happen here."""
     world = dist.get_world_size(group)
     dev = rows.device
     wire = _wire_device(dev, group)
-    sc = torch.tensor(send_counts, dtype=torch.int64, device=wire)
-    rc = torch.empty(world, dtype=torch.int64, device=wire)
-    dist.all_to_all_single(rc, sc, group=group)
-    recv_counts = rc.cpu().tolist()
-    shape = (sum(recv_counts),) + tuple(rows.shape[1:])
+    if recv_counts is None:
+        sc = torch.tensor(list(send_counts), dtype=torch.int64, device=wire)
+        rc = torch.empty(world, dtype=torch.int64, device=wire)
+        dist.all_to_all_single(rc, sc, group=group)
+        recv_counts = rc.cpu().tolist()
+    shape = (int(sum(recv_counts)),) + tuple(rows.shape[1:])
     out = torch.empty(shape, dtype=rows.dtype, device=wire)
-    dist.all_to_all_single(out, rows.contiguous().to(wire), output_split_sizes=recv_counts,
-                           input_split_sizes=list(send_counts), group=group)
+    dist.all_to_all_single(out, rows.contiguous().to(wire), output_split_sizes=[int(c) for c in recv_counts],
+                           input_split_sizes=[int(c) for c in send_counts], group=group)
     return out.to(dev)
 
 
@@ -228,55 +256,101 @@ def _exclusive_offsets(n_locals, group, device):
     return [(sum(row[k] for row in allc[:r]), sum(row[k] for row in allc)) for k in range(len(n_locals))]
 
 
+def check_slab_halo(shape, offsets, own_begin, own_end):
+    """The slab layout gives every rank the planes below its owned range as a
+    lower halo and nothing above it.  An affinity sample aff[c, p] needs the
+    partner p + o_c: with a lower neighbour (own_begin[0] > 0) the halo must
+    hold max(-o_z) planes, and positive z offsets have no upper halo at all;
+    x / y are never split.  Raise instead of silently dropping samples."""
+    if offsets is None:
+        return
+    off = np.asarray(offsets, dtype=np.int64).reshape(-1, 3)
+    ob = int(own_begin[0]) if own_begin is not None else 0
+    oe = int(own_end[0]) if own_end is not None else int(shape[0])
+    need_lo = int(max(0, -off[:, 0].min())) if off.size else 0
+    if ob > 0 and ob < need_lo:
+        raise ValueError('slab halo of %d plane(s) below the owned range, but the affinity offsets reach %d '
+                         'planes down: give each rank max(-offset_z) halo planes' % (ob, need_lo))
+    if off.size and off[:, 0].max() > 0 and oe < int(shape[0]) + int(off[:, 0].max()):
+        raise ValueError('positive z offsets need an upper halo, which the z-slab layout does not have')
+
+
 def rag_features_distributed(labels, data=None, offsets=None, own_begin=None, own_end=None,
                              ignore_label=False, hist_range=(0.0, 1.0), group=None, backend=None):
     """Global RAG + edge features of a z-slab-partitioned volume.
 
-    Every rank passes its slab (plus the halo plane below it, excluded via
+    Every rank passes its slab (plus the halo planes below it, excluded via
     ``own_begin``); the call is collective.  Returns a ``DistResult`` whose
     edge rows are rows [edge_offset, edge_offset + n_edges) of the global
     sorted edge table (same for nodes).
+
+    Collectives: one all_gather of the splitter samples, one all_gather of
+    the (edge, node) send-count matrix -- the only host round trip before the
+    data moves --, one all_to_all of edge rows, one of node ids, and the
+    all_gather of the shard sizes.  Splitters and counts are computed on the
+    wire device, so with RCCL nothing but the count matrix leaves HBM.
     """
+    shape = tuple(labels.shape)
+    if world_size_of(group) > 1:
+        check_slab_halo(shape, offsets, own_begin, own_end)
     backend = backend or HipBackend()
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     keys, sums, recs, nodes, info, feats = backend.local(labels, data, offsets, own_begin, own_end,
                                                          ignore_label, hist_range)
     dev = keys.device
+    wire = _wire_device(dev, group)
     n = keys.shape[0]
-    # splitters on u from an evenly spaced sample of the sorted local keys; the
-    # largest label rides along (packed (u,v) keys need labels < 2^31)
+    nodes = nodes.reshape(-1)
+    # splitters on u (unsigned order) from an evenly spaced sample of the
+    # sorted local keys; the signed min / max of every label ride along
+    # (the packed (u,v) fast path needs 0 <= label < 2^31)
+    ou = _ordered(keys[:, 0]) if n else keys[:, 0]
     if n > 0:
         idx = torch.div(torch.arange(N_SAMPLES, device=dev, dtype=torch.int64) * n, N_SAMPLES,
                         rounding_mode='floor')
-        samp = keys[:, 0].index_select(0, idx)
-        vmax = keys[:, 1].max().reshape(1)
+        samp = ou.index_select(0, idx)
+        lo = torch.minimum(keys.min(), nodes.min() if nodes.numel() else keys.min()).reshape(1)
+        hi = torch.maximum(keys.max(), nodes.max() if nodes.numel() else keys.max()).reshape(1)
     else:
         samp = torch.zeros(N_SAMPLES, dtype=torch.int64, device=dev)
-        vmax = torch.zeros(1, dtype=torch.int64, device=dev)
-    meta = torch.cat([samp, torch.tensor([n], dtype=torch.int64, device=dev), vmax])
-    g = torch.stack(all_gather_tensor(meta, group)).cpu().numpy()
-    splitters = weighted_splitters(g[:, :N_SAMPLES], g[:, N_SAMPLES], world)
-    counts = split_counts(keys[:, 0], splitters)
-    packable = int(g[:, N_SAMPLES + 1].max()) < (1 << 31) and int(nodes.max().item() if nodes.numel() else 0) < (1 << 31)
+        z = nodes.min().reshape(1) if nodes.numel() else torch.zeros(1, dtype=torch.int64, device=dev)
+        lo = z
+        hi = nodes.max().reshape(1) if nodes.numel() else z
+    meta = torch.cat([samp, torch.tensor([n], dtype=torch.int64, device=dev), lo, hi]).to(wire)
+    g = torch.stack(all_gather_tensor(meta, group))
+    splitters = weighted_splitters_t(g[:, :N_SAMPLES], g[:, N_SAMPLES], world)
+    packable = torch.logical_and(g[:, N_SAMPLES + 1].min() >= 0, g[:, N_SAMPLES + 2].max() < (1 << 31))
+    onodes = _ordered(nodes)
+    e_counts = split_counts_t(ou.to(wire), splitters)
+    n_counts = split_counts_t(onodes.to(wire), splitters)
+    mine = torch.cat([e_counts, n_counts, packable.reshape(1).to(torch.int64)])
+    cm = torch.stack(all_gather_tensor(mine, group)).cpu()         # (world, 2*world + 1): the host round trip
+    packable = bool(cm[:, 2 * world].min().item())
+    e_send = cm[rank, :world].tolist()
+    n_send = cm[rank, world:2 * world].tolist()
+    e_recv_all = cm[:, rank].tolist()
+    n_recv = cm[:, world + rank].tolist()
 
     if not packable:
         # general labels: every row goes to the owner of its u and is merged there
         rows = pack_rows(keys, sums, recs)
-        recv = exchange(rows, counts, group)
+        recv = exchange(rows, e_send, group, recv_counts=e_recv_all)
         rk, rs, rr = unpack_rows(recv)
         me, mf = backend.merge(rk, rs, rr, hist_range)
         merged = {'edges': me, 'features': mf}
     else:
         # rows of other owners leave; this rank's own block stays in place
-        lo = sum(counts[:rank])
-        hi = lo + counts[rank]
-        send = list(counts)
+        lo_i = sum(e_send[:rank])
+        hi_i = lo_i + e_send[rank]
+        send = list(e_send)
         send[rank] = 0
-        out_k = torch.cat([keys[:lo], keys[hi:]])
-        out_rows = pack_rows(out_k, torch.cat([sums[:lo], sums[hi:]]), torch.cat([recs[:lo], recs[hi:]]))
-        recv = exchange(out_rows, send, group)
-        lk, ls, lr, lf = keys[lo:hi], sums[lo:hi], recs[lo:hi], feats[lo:hi]
+        recv_counts = list(e_recv_all)
+        recv_counts[rank] = 0
+        out_k = torch.cat([keys[:lo_i], keys[hi_i:]])
+        out_rows = pack_rows(out_k, torch.cat([sums[:lo_i], sums[hi_i:]]), torch.cat([recs[:lo_i], recs[hi_i:]]))
+        recv = exchange(out_rows, send, group, recv_counts=recv_counts)
+        lk, ls, lr, lf = keys[lo_i:hi_i], sums[lo_i:hi_i], recs[lo_i:hi_i], feats[lo_i:hi_i]
         if recv.shape[0] == 0:
             shared = torch.zeros(lk.shape[0], dtype=torch.bool, device=dev)
         else:
@@ -297,9 +371,13 @@ def rag_features_distributed(labels, data=None, offsets=None, own_begin=None, ow
             merged = _merge_sorted(lk[keep], lf[keep], me, mf)
     n_loc = int(merged['edges'].shape[0])
 
-    # nodes -> the same ranges
-    nrecv = exchange(nodes.reshape(-1), split_counts(nodes.reshape(-1), splitters), group)
+    # nodes -> the same ranges (send counts known from the count matrix)
+    nrecv = exchange(nodes, n_send, group, recv_counts=n_recv)
     node_shard = backend.unique(nrecv)
 
     (e_off, e_tot), (n_off, n_tot) = _exclusive_offsets([n_loc, int(node_shard.shape[0])], group, dev)
     return DistResult(merged, node_shard, e_off, e_tot, n_off, n_tot, info)
+
+
+def world_size_of(group):
+    return dist.get_world_size(group) if dist.is_initialized() else 1

@@ -16,6 +16,14 @@ ndist mirror needs its own codec.  Format (N5 spec 2.0, as written by z5):
 * ``read_chunk`` of a missing chunk returns None (test_graph.py:63-66,
   block_edge_features.py:181-185); ``write_chunk(pos, data, True)`` writes a
   varlength chunk (block_edge_features.py:236).
+
+zarr v2 containers (``.zr`` / ``.zarr``, accepted by graph_workflow.py:17-20
+and features_workflow.py:24-29 for the input volumes) are read and written by
+the same classes: ``.zgroup`` / ``.zarray`` / ``.zattrs`` metadata in C axis
+order, chunk keys ``i.j.k`` (or ``i/j/k`` with dimension_separator "/"),
+edge chunks stored at full chunk shape, missing chunks = fill_value, and the
+gzip / zlib / uncompressed codecs.  Blosc (zarr's default codec) needs the
+c-blosc library, which this image does not have: such arrays raise on access.
 """
 from __future__ import annotations
 
@@ -32,31 +40,49 @@ _ATTR = 'attributes.json'
 _lock = threading.Lock()
 
 
-def _read_json(path):
-    p = os.path.join(path, _ATTR)
+def _read_json(path, name=_ATTR):
+    p = os.path.join(path, name)
     if not os.path.exists(p):
         return {}
     with open(p) as f:
         return json.load(f)
 
 
-def _write_json(path, d):
+def _write_json(path, d, name=_ATTR):
     os.makedirs(path, exist_ok=True)
-    tmp = os.path.join(path, _ATTR + '.tmp%d' % os.getpid())
+    tmp = os.path.join(path, name + '.tmp%d_%d' % (os.getpid(), threading.get_ident()))
     with open(tmp, 'w') as f:
         json.dump(d, f)
-    os.replace(tmp, os.path.join(path, _ATTR))
+    os.replace(tmp, os.path.join(path, name))
+
+
+_ZGROUP, _ZARRAY, _ZATTRS = '.zgroup', '.zarray', '.zattrs'
+
+
+def is_container_root(path):
+    """True for the root directory of an N5 or zarr container."""
+    if not os.path.isdir(path):
+        return False
+    if path.rstrip('/').lower().endswith(('.n5', '.zr', '.zarr')):
+        return True
+    return 'n5' in _read_json(path)
+
+
+def _is_zarr_path(path):
+    return path.rstrip('/').split('.')[-1].lower() in ('zr', 'zarr')
 
 
 class Attributes:
-    """dict-like view of the user attributes stored in attributes.json."""
+    """dict-like view of the user attributes (N5: inside attributes.json,
+    zarr: .zattrs)."""
     _RESERVED = ('dimensions', 'blockSize', 'dataType', 'compression', 'n5')
 
-    def __init__(self, path):
+    def __init__(self, path, name=_ATTR):
         self.path = path
+        self.name = name
 
     def _load(self):
-        return _read_json(self.path)
+        return _read_json(self.path, self.name)
 
     def __getitem__(self, k):
         return self._load()[k]
@@ -74,7 +100,7 @@ class Attributes:
         with _lock:
             d = self._load()
             d[k] = v
-            _write_json(self.path, d)
+            _write_json(self.path, d, self.name)
 
     def __contains__(self, k):
         return k in self._load()
@@ -225,7 +251,7 @@ class Dataset:
 
     def __getitem__(self, index):
         bb, squeeze = self._norm_index(index)
-        out = np.zeros(tuple(e - b for b, e in bb), dtype=self.dtype)
+        out = np.full(tuple(e - b for b, e in bb), getattr(self, 'fill_value', 0), dtype=self.dtype)
 
         def one(pos):
             data = self.read_chunk(pos)
@@ -282,11 +308,83 @@ class Dataset:
                 one(c)
 
 
+_ZARR_CODECS = ('gzip', 'zlib')
+
+
+class ZarrArray(Dataset):
+    """A zarr v2 array with the Dataset interface (C axis order)."""
+
+    def __init__(self, path):
+        self.path = path
+        meta = _read_json(path, _ZARRAY)
+        if 'shape' not in meta:
+            raise KeyError('%s is not a zarr array' % path)
+        if meta.get('order', 'C') != 'C':
+            raise ValueError('zarr array %s: only C order is supported' % path)
+        if meta.get('filters'):
+            raise ValueError('zarr array %s: filters are not supported' % path)
+        self.shape = tuple(int(x) for x in meta['shape'])
+        self.chunks = tuple(int(x) for x in meta['chunks'])
+        self.dtype = np.dtype(meta['dtype'])
+        self.fill_value = meta.get('fill_value', 0) or 0
+        self.compressor = meta.get('compressor')
+        self.sep = meta.get('dimension_separator', '.')
+        self.attrs = Attributes(path, _ZATTRS)
+        self.n_threads = 1
+
+    def _codec(self):
+        c = self.compressor
+        if c is None:
+            return None
+        cid = c.get('id')
+        if cid not in _ZARR_CODECS:
+            raise ValueError('zarr array %s: compressor %r is not available in this image (gzip, zlib or none '
+                             'are supported)' % (self.path, cid))
+        return cid
+
+    def _chunk_path(self, pos):
+        return os.path.join(self.path, self.sep.join(str(int(p)) for p in pos))
+
+    def write_chunk(self, pos, data, varlen=False):
+        if varlen:
+            raise ValueError('zarr has no varlength chunks (the sub-graph datasets are N5)')
+        pos = tuple(int(p) for p in pos)
+        data = np.asarray(data, dtype=self.dtype)
+        full = np.full(self.chunks, self.fill_value, dtype=self.dtype)
+        full[tuple(slice(0, n) for n in data.shape)] = data
+        raw = np.ascontiguousarray(full).tobytes()
+        cid = self._codec()
+        level = (self.compressor or {}).get('level', 5)
+        if cid == 'gzip':
+            co = zlib.compressobj(level, zlib.DEFLATED, 16 + zlib.MAX_WBITS)
+            raw = co.compress(raw) + co.flush()
+        elif cid == 'zlib':
+            raw = zlib.compress(raw, level)
+        p = self._chunk_path(pos)
+        os.makedirs(os.path.dirname(p), exist_ok=True)
+        tmp = p + '.tmp%d_%d' % (os.getpid(), threading.get_ident())
+        with open(tmp, 'wb') as f:
+            f.write(raw)
+        os.replace(tmp, p)
+
+    def read_chunk(self, pos):
+        p = self._chunk_path(pos)
+        if not os.path.exists(p):
+            return None
+        with open(p, 'rb') as f:
+            buf = f.read()
+        raw = _decompress(buf) if self._codec() else buf
+        arr = np.frombuffer(raw, dtype=self.dtype).reshape(self.chunks)
+        cs = self._chunk_shape(tuple(int(x) for x in pos))
+        return np.ascontiguousarray(arr[tuple(slice(0, n) for n in cs)])
+
+
 class Group:
-    def __init__(self, path, mode='a'):
+    def __init__(self, path, mode='a', zarr=False):
         self.path = path
         self.mode = mode
-        self.attrs = Attributes(path)
+        self.zarr = zarr
+        self.attrs = Attributes(path, _ZATTRS if zarr else _ATTR)
 
     def __contains__(self, key):
         return os.path.isdir(os.path.join(self.path, key))
@@ -295,6 +393,10 @@ class Group:
         p = os.path.join(self.path, key)
         if not os.path.isdir(p):
             raise KeyError(key)
+        if self.zarr:
+            if os.path.exists(os.path.join(p, _ZARRAY)):
+                return ZarrArray(p)
+            return Group(p, self.mode, True)
         meta = _read_json(p)
         if 'dimensions' in meta:
             return Dataset(p)
@@ -303,14 +405,27 @@ class Group:
     def keys(self):
         return sorted(d for d in os.listdir(self.path) if os.path.isdir(os.path.join(self.path, d)))
 
+    def _make_group_dirs(self, p):
+        if self.zarr:
+            # every intermediate level is a zarr group
+            rel = os.path.relpath(p, self.path).split(os.sep)
+            cur = self.path
+            for part in rel:
+                cur = os.path.join(cur, part)
+                os.makedirs(cur, exist_ok=True)
+                if not os.path.exists(os.path.join(cur, _ZGROUP)):
+                    _write_json(cur, {'zarr_format': 2}, _ZGROUP)
+        else:
+            os.makedirs(p, exist_ok=True)
+            _write_json(p, _read_json(p))
+
     def require_group(self, key):
         p = os.path.join(self.path, key)
         if not os.path.isdir(p):
             if self.mode == 'r':
                 raise ValueError('read-only container')
-            os.makedirs(p, exist_ok=True)
-            _write_json(p, _read_json(p))
-        return Group(p, self.mode)
+            self._make_group_dirs(p)
+        return Group(p, self.mode, self.zarr)
 
     create_group = require_group
 
@@ -323,19 +438,34 @@ class Group:
         chunks = tuple(int(c) for c in (chunks if chunks is not None else shape))
         chunks = tuple(max(1, c) for c in chunks)
         p = os.path.join(self.path, key)
-        meta = _read_json(p)
-        meta.update({'dimensions': list(shape[::-1]), 'blockSize': list(chunks[::-1]),
-                     'dataType': np.dtype(dtype).name, 'compression': _normalize_compression(compression)})
-        _write_json(p, meta)
-        ds = Dataset(p)
+        parent = os.path.dirname(p)
+        if parent != self.path and not os.path.isdir(parent):
+            self._make_group_dirs(parent)
+        if self.zarr:
+            comp = _normalize_compression(compression)
+            zc = None if comp['type'] == 'raw' else {'id': 'zlib' if comp.get('useZlib') else 'gzip',
+                                                     'level': comp.get('level', 5)}
+            os.makedirs(p, exist_ok=True)
+            _write_json(p, {'zarr_format': 2, 'shape': list(shape), 'chunks': list(chunks),
+                            'dtype': np.dtype(dtype).str, 'compressor': zc, 'fill_value': 0, 'order': 'C',
+                            'filters': None}, _ZARRAY)
+            ds = ZarrArray(p)
+        else:
+            meta = _read_json(p)
+            meta.update({'dimensions': list(shape[::-1]), 'blockSize': list(chunks[::-1]),
+                         'dataType': np.dtype(dtype).name, 'compression': _normalize_compression(compression)})
+            _write_json(p, meta)
+            ds = Dataset(p)
         if data is not None:
             ds[...] = data
         return ds
 
     def require_dataset(self, key, shape, chunks=None, dtype=None, compression='gzip', **kw):
         p = os.path.join(self.path, key)
-        if os.path.isdir(p) and 'dimensions' in _read_json(p):
-            ds = Dataset(p)
+        exists = os.path.exists(os.path.join(p, _ZARRAY)) if self.zarr else \
+            (os.path.isdir(p) and 'dimensions' in _read_json(p))
+        if exists:
+            ds = ZarrArray(p) if self.zarr else Dataset(p)
             if tuple(ds.shape) != tuple(int(s) for s in shape):
                 raise ValueError('shape mismatch for existing dataset %s' % key)
             return ds
@@ -343,18 +473,24 @@ class Group:
 
 
 class File(Group):
-    """z5py.File-like N5 container (context manager)."""
+    """z5py.File-like N5 (or, for a .zr / .zarr path, zarr v2) container
+    (context manager)."""
 
-    def __init__(self, path, mode='a'):
+    def __init__(self, path, mode='a', use_zarr_format=None):
+        zarr = _is_zarr_path(path) if use_zarr_format is None else bool(use_zarr_format)
         if mode != 'r':
             os.makedirs(path, exist_ok=True)
-            meta = _read_json(path)
-            if 'n5' not in meta:
-                meta['n5'] = '2.0.0'
-                _write_json(path, meta)
+            if zarr:
+                if not os.path.exists(os.path.join(path, _ZGROUP)):
+                    _write_json(path, {'zarr_format': 2}, _ZGROUP)
+            else:
+                meta = _read_json(path)
+                if 'n5' not in meta:
+                    meta['n5'] = '2.0.0'
+                    _write_json(path, meta)
         elif not os.path.isdir(path):
-            raise OSError('no N5 container at %s' % path)
-        super().__init__(path, mode)
+            raise OSError('no %s container at %s' % ('zarr' if zarr else 'N5', path))
+        super().__init__(path, mode, zarr)
 
     def __enter__(self):
         return self
@@ -367,8 +503,9 @@ class File(Group):
 
 
 def file_reader(path, mode='a'):
-    """vu.file_reader (utils/volume_utils.py:21-22) restricted to N5."""
+    """vu.file_reader (utils/volume_utils.py:21-22) for the formats the hot path
+    accepts (graph_workflow.py:17-20): N5 (.n5) and zarr (.zr / .zarr)."""
     ending = path.rstrip('/').split('.')[-1].lower()
-    if ending not in ('n5',):
-        raise ValueError('only N5 containers are supported by this codec, got %s' % path)
+    if ending not in ('n5', 'zr', 'zarr'):
+        raise ValueError('only N5 and zarr containers are supported, got %s' % path)
     return File(path, mode)

@@ -35,14 +35,30 @@ from . import rag
 from .blocking import blocking
 
 N_FEATURES = 10
-STATS_SUFFIX = '_stats'   # companion varlen dataset: per edge (sum, sumsq, 48 record words)
-STATS_WIDTH = 2 + rag.WIDE_WORDS
+# companion varlen dataset of sub_features (uint32): per edge the (sum, sumsq)
+# float64 pair as 4 words, then the 48 words of the wide statistics record
+# (42 histogram slots, count|ADJ, ordered min, ordered max, pad) = 208 B
+STATS_SUFFIX = '_stats'
+STATS_WORDS = 4 + rag.WIDE_WORDS
 ORD_POS_INF = 0xFF800000   # order-preserving u32 code of +inf (ctg_internal.h f2ord)
 ORD_NEG_INF = 0x007FFFFF   # ... of -inf
 
 
 def _open(path, mode='a'):
-    return n5.File(path, mode)
+    return n5.file_reader(path, mode)
+
+
+def _split_container_path(path):
+    """'/data/problem.n5/s0/graph' -> ('/data/problem.n5', 's0/graph'): the
+    single-path form of ndist.Graph (ilastik/carving.py:28,
+    edges_from_skeletons.py:146) names a group inside a container."""
+    p = os.path.abspath(path)
+    parts = p.split(os.sep)
+    for i in range(len(parts), 0, -1):
+        root = os.sep.join(parts[:i]) or os.sep
+        if n5.is_container_root(root):
+            return root, '/'.join(parts[i:])
+    raise ValueError('%s is not inside an N5 / zarr container' % path)
 
 
 def _map(fn, items, n_threads):
@@ -122,12 +138,15 @@ def mergeSubgraphs(graphPath, subgraphKey, blockIds, outKey, numberOfThreads=1, 
         else:
             edges = np.zeros((0, 2), np.uint64)
         if serializeToVarlen:
+            # merge_sub_graphs.py:140-152: the old-scale blocks tile one block
+            # of the coarser grid; its lower corner is the elementwise minimum
+            # of their begins, whatever order the ids come in
+            if not block_ids:
+                return
             out = f[outKey]
             out_chunks = out['nodes'].chunks
-            first = blk.getBlock(block_ids[0]) if block_ids else None
-            if first is None:
-                return
-            pos = [b // c for b, c in zip(first.begin, out_chunks)]
+            begins = np.array([blk.getBlock(b).begin for b in block_ids], dtype=np.int64)
+            pos = [int(b) // c for b, c in zip(begins.min(axis=0), out_chunks)]
             out['nodes'].write_chunk(pos, nodes, True)
             if edges.shape[0]:
                 out['edges'].write_chunk(pos, edges.ravel(), True)
@@ -246,22 +265,45 @@ def mapEdgeIds(graphPath, graphKey, subgraphKey, blockIds, numberOfThreads=1):  
 class Graph:
     """ndist.Graph: a graph over arbitrary uint64 node ids.
 
-    Graph(edges) | Graph(path, key, numberOfThreads=n).  numberOfNodes is the
-    count of distinct nodes (test_graph.py:80-81, reduce_problem.py:322-326).
+    Constructor forms used by the reference and its consumers:
+      Graph(edges)                          test_graph.py:68, block_edge_features.py:187
+      Graph(path, key[, numberOfThreads=n]) test_graph.py:32,111, solve_subproblems.py:250
+      Graph(path_with_key)                  ilastik/carving.py:28
+      Graph(path_with_key, n_threads)       edges_from_skeletons.py:146
+    numberOfNodes is the count of distinct nodes: a block sub-graph may have
+    fewer nodes than gridRag's max+1 (test_graph.py:78-80), and the scale-0
+    consumer sizes its node arrays by len(nodes) (reduce_problem.py:322-326).
+    For the dense 0..max labels of the reference's test data this equals
+    seg.max()+1 (test_graph.py:113).
     """
 
     def __init__(self, *args, numberOfThreads=1):  # noqa: N803
         nodes = None
-        if len(args) == 1 and not isinstance(args[0], str):
+        if len(args) == 1 and not isinstance(args[0], (str, os.PathLike)):
             edges = np.asarray(args[0], dtype=np.uint64).reshape(-1, 2)
-        elif len(args) >= 2:
-            with _open(args[0], 'r') as f:
-                g = f[args[1]]
-                edges = g['edges'][:] if 'edges' in g else np.zeros((0, 2), np.uint64)
+        elif 1 <= len(args) <= 3 and isinstance(args[0], (str, os.PathLike)):
+            if len(args) >= 2 and isinstance(args[1], str):
+                path, key = str(args[0]), args[1]
+                rest = args[2:]
+            else:
+                path, key = _split_container_path(str(args[0]))
+                rest = args[1:]
+            if rest:
+                numberOfThreads = int(rest[0])  # noqa: N806
+            with _open(path, 'r') as f:
+                g = f[key] if key else f
+                if 'edges' in g:
+                    ds = g['edges']
+                    ds.n_threads = max(1, int(numberOfThreads))
+                    edges = ds[:]
+                else:
+                    edges = np.zeros((0, 2), np.uint64)
                 if 'nodes' in g:
-                    nodes = g['nodes'][:]
+                    ds = g['nodes']
+                    ds.n_threads = max(1, int(numberOfThreads))
+                    nodes = ds[:]
         else:
-            raise TypeError('Graph(edges) or Graph(path, key)')
+            raise TypeError('Graph(edges), Graph(path, key[, numberOfThreads]) or Graph(path_with_key[, n_threads])')
         self._uv = np.ascontiguousarray(edges.reshape(-1, 2).astype(np.uint64))
         self._nodes = np.unique(self._uv) if nodes is None else np.asarray(nodes, dtype=np.uint64)
         self._sorted = None
@@ -357,15 +399,28 @@ class Graph:
 # features
 # ---------------------------------------------------------------------------
 
+def _stats_dataset(fo, outKey, shape, chunks):  # noqa: N803
+    return fo.require_dataset(outKey + STATS_SUFFIX, shape=shape, chunks=chunks, dtype='uint32',
+                              compression='gzip')
+
+
+def encode_stats_words(sums, records):
+    """(E,2) float64 sums + (E,48) uint32 records -> (E,52) uint32 words."""
+    n = records.shape[0]
+    out = np.empty((n, STATS_WORDS), dtype=np.uint32)
+    out[:, :4] = np.ascontiguousarray(sums, dtype=np.float64).view(np.uint32).reshape(n, 4)
+    out[:, 4:] = records
+    return out
+
+
+def decode_stats_words(words):
+    w = np.ascontiguousarray(words, dtype=np.uint32).reshape(-1, STATS_WORDS)
+    return np.ascontiguousarray(w[:, :4]).view(np.float64).reshape(-1, 2), np.ascontiguousarray(w[:, 4:])
+
+
 def _write_block_features(fo, outKey, pos, shape, chunks, feats, sums, records):  # noqa: N803
-    ds = fo[outKey]
-    ds.write_chunk(pos, feats.ravel(), True)
-    st = fo.require_dataset(outKey + STATS_SUFFIX, shape=shape, chunks=chunks, dtype='float64',
-                            compression='gzip')
-    stats = np.zeros((feats.shape[0], STATS_WIDTH), dtype=np.float64)
-    stats[:, :2] = sums
-    stats[:, 2:] = records.astype(np.float64)
-    st.write_chunk(pos, stats.ravel(), True)
+    fo[outKey].write_chunk(pos, feats.ravel(), True)
+    _stats_dataset(fo, outKey, shape, chunks).write_chunk(pos, encode_stats_words(sums, records).ravel(), True)
 
 
 def _block_features(graphPath, subgraphKey, dataPath, dataKey, labelsPath, labelsKey, blockIds,  # noqa: N803
@@ -451,41 +506,55 @@ def extractBlockFeaturesFromAffinityMaps_uint8(*args, **kw):  # noqa: N802
 def mergeFeatureBlocks(graphPath, subgraphKey, featuresPath, featuresKey, outPath, outKey,  # noqa: N802,N803
                        blockIds, edgeIdBegin, edgeIdEnd, numberOfThreads=1):  # noqa: N803
     """Combine the per-block feature rows of edges in [edgeIdBegin, edgeIdEnd)
-    into rows of the (E,10) ``outKey`` dataset: counts add, mean count-weighted,
-    variance by Chan's formula, min/max over non-empty blocks, quantiles from
-    the merged histograms (exact; SURVEY OPEN-3 default)."""
+    into rows of the (E,10) ``outKey`` dataset.
+
+    Blocks written by this library carry the mergeable statistics in the
+    ``<featuresKey>_stats`` companion (uint32, 52 words per edge): counts and
+    sums add, min/max elementwise, histograms add, and the quantiles are those
+    of the merged histogram -- identical to the whole-volume features (SURVEY
+    OPEN-3 default).  Reference-layout ``sub_features`` (10 float64 columns per
+    row, no companion, e.g. written by nifty) are merged from the rows alone
+    (``ctg_merge_feature_rows``): count sum, count-weighted mean, the exact
+    pooled variance of the block (count, mean, var) triples, min/max over
+    non-empty rows, and count-weighted quantiles (nifty-compatible; the exact
+    merged quantiles need the histograms)."""
     begin, end = int(edgeIdBegin), int(edgeIdEnd)
     with _open(graphPath, 'r') as fg, _open(featuresPath, 'r') as ff:
         g = fg[subgraphKey]
         blk, _ = _subgraph_blocking(g)
         ds_ids = g['edge_ids']
-        if featuresKey + STATS_SUFFIX not in ff:
-            raise RuntimeError('mergeFeatureBlocks: %s has no %s companion dataset; the block features were '
-                               'not written by cluster_tools_amd' % (featuresKey, STATS_SUFFIX))
-        ds_st = ff[featuresKey + STATS_SUFFIX]
+        have_stats = featuresKey + STATS_SUFFIX in ff
+        ds_feat = ff[featuresKey + STATS_SUFFIX] if have_stats else ff[featuresKey]
+        width = STATS_WORDS if have_stats else N_FEATURES
 
         def load(b):
             pos = blk.blockGridPosition(int(b))
             ids = ds_ids.read_chunk(pos)
             if ids is None:
                 return None
-            st = ds_st.read_chunk(pos)
-            if st is None:
+            rows = ds_feat.read_chunk(pos)
+            if rows is None:
                 return None
-            st = st.reshape(-1, STATS_WIDTH)
+            rows = rows.reshape(-1, width)
+            if rows.shape[0] != ids.shape[0]:
+                raise RuntimeError('mergeFeatureBlocks: block %d has %d edge ids but %d feature rows'
+                                   % (int(b), ids.shape[0], rows.shape[0]))
             sel = (ids >= begin) & (ids < end)
-            return ids[sel], st[sel]
+            return ids[sel], rows[sel]
 
         parts = [p for p in _map(load, blockIds, numberOfThreads) if p is not None and len(p[0])]
     out = np.zeros((end - begin, N_FEATURES), np.float64)
     if parts:
         ids = np.concatenate([p[0] for p in parts]).astype(np.uint64)
-        st = np.concatenate([p[1] for p in parts], axis=0)
-        keys = np.zeros((ids.shape[0], 2), np.uint64)
-        keys[:, 1] = ids
-        recs = st[:, 2:].astype(np.uint32)
-        recs[:, 42] |= np.uint32(0x80000000)   # every block row is a graph edge
-        merged = rag.merge_stats(keys, st[:, :2], recs)
-        out[merged['edges'][:, 1].astype(np.int64) - begin] = merged['features']
+        rows = np.concatenate([p[1] for p in parts], axis=0)
+        if have_stats:
+            sums, recs = decode_stats_words(rows)
+            keys = np.zeros((ids.shape[0], 2), np.uint64)
+            keys[:, 1] = ids
+            recs[:, 42] |= np.uint32(0x80000000)   # every block row is a graph edge
+            merged = rag.merge_stats(keys, sums, recs)
+            out[merged['edges'][:, 1].astype(np.int64) - begin] = merged['features']
+        else:
+            out = rag.merge_feature_rows(ids, rows, begin, end)
     with _open(outPath) as fo:
         fo[outKey][begin:end, :] = out

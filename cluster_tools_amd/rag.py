@@ -300,6 +300,21 @@ def merge_stats(keys, sums, records, hist_range=(0.0, 1.0), keep_stats=False):
     return out
 
 
+def merge_feature_rows(ids, rows, id_begin, id_end):
+    """Reference-layout (n,10) feature rows of global edge ids -> the merged
+    (id_end - id_begin, 10) rows (ctg_merge_feature_rows)."""
+    lib = L.load()
+    L.init_device()
+    ids = np.ascontiguousarray(np.asarray(ids, dtype=np.uint64).reshape(-1))
+    rows = np.ascontiguousarray(np.asarray(rows, dtype=np.float64).reshape(-1, N_FEATURES))
+    if rows.shape[0] != ids.shape[0]:
+        raise ValueError('ids and rows differ in length')
+    out = np.zeros((int(id_end) - int(id_begin), N_FEATURES), dtype=np.float64)
+    L.check(lib.ctg_merge_feature_rows(_ptr(ids), _ptr(rows), ids.shape[0], int(id_begin), int(id_end), _ptr(out),
+                                       L.CTG_MEM_HOST, None), 'ctg_merge_feature_rows')
+    return out
+
+
 def unique_pairs(pairs):
     """Sorted unique rows of an (n,2) uint64 pair list -> (edges, nodes)."""
     lib = L.load()
@@ -352,6 +367,12 @@ def synth_affinities(boundary, offsets):
                                   ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
     L.check(rc, 'ctg_synth_affinities')
     return affs
+
+
+def trim_cache():
+    """Return the library's cached device memory (workspace + pool) to HIP."""
+    L.init_device()
+    L.check(L.load().ctg_trim(), 'ctg_trim')
 
 
 def set_profiling(on=True):

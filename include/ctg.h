@@ -22,6 +22,9 @@
  *                                        graph/map_edge_ids.py:116-119, test/graph/test_graph.py:92
  *   ctg_unique_labels                 <- the per-block ``nodes`` of computeMergeableRegionGraph
  *                                        test/graph/test_graph.py:53-60
+ *   ctg_merge_feature_rows            <- ndist.mergeFeatureBlocks on reference-layout
+ *                                        (10-column) sub_features rows,
+ *                                        features/merge_edge_features.py:141-147
  *
  * Conventions: plain pointers and sizes; ``mem`` says whether array
  * arguments live in host memory (CTG_MEM_HOST) or in device memory of the
@@ -113,6 +116,14 @@ int ctg_merge_stats(const uint64_t* keys, const double* sums, const uint32_t* re
                     int64_t n, double hist_lo, double hist_hi, int keep_stats,
                     int mem, void* stream, ctg_result** out);
 
+/* Merge reference-layout feature rows (n x 10 float64, [mean, var, min,
+ * q10..q90, max, count]) of global edges ids[i] in [id_begin, id_end) into
+ * out ((id_end - id_begin) x 10): count sum, count-weighted mean, exact pooled
+ * variance, min / max over rows with count > 0, count-weighted quantiles.
+ * Edges without rows get zero rows.  An id outside the range is CTG_ERR_ARG. */
+int ctg_merge_feature_rows(const uint64_t* ids, const double* rows, int64_t n, int64_t id_begin, int64_t id_end,
+                           double* out, int mem, void* stream);
+
 /* sorted unique (u,v) pairs of an (n,2) uint64 list (union of block sub-graph
  * edge lists, ndist.mergeSubgraphs); result nodes = unique endpoints */
 int ctg_unique_pairs(const uint64_t* pairs, int64_t n, int mem, void* stream, ctg_result** out);
@@ -141,6 +152,10 @@ int ctg_synth_volume(uint64_t* labels, float* boundary, const int64_t* shape,
                      uint64_t seed, uint64_t label_offset, double noise_amp, void* stream);
 int ctg_synth_affinities(const float* boundary, float* affs, const int64_t* shape,
                          int n_channels, const int32_t* offsets, void* stream);
+
+/* release every device block the library caches on the current device
+ * (workspace and allocator pool); result handles stay valid */
+int ctg_trim(void);
 
 /* profiling: per-phase device milliseconds of the last ctg_rag_features call
  * (HIP events on the call's stream): [0] face scan, [1] key pack, [2] sort,

@@ -28,11 +28,17 @@ def _free_port():
 
 
 BIG = 1 << 33   # labels >= 2^31: the exchange falls back to merging every row
+HUGE = (1 << 63) + 5   # labels >= 2^63: negative in the int64 views on the wire
 
 
 def _volume(shape, cell, big):
     lab, bnd = synthetic.generate(shape, cell=cell, seed=3)
-    if big:
+    if big == 'flat_top':
+        # the top half is one label: the upper ranks own no edge at all
+        lab[shape[0] // 2:] = lab.max() + 1
+    elif big == 'huge':
+        lab = lab + np.uint64(HUGE)
+    elif big:
         lab = lab + np.uint64(BIG)
     return lab, bnd
 
@@ -63,6 +69,11 @@ def _worker(rank, world, port, shape, cell, outdir, ignore_label, big=False):
     (2, (24, 40, 36), 6, False, False),
     (3, (30, 33, 29), 5, True, False),
     (2, (20, 30, 28), 5, False, True),
+    (4, (32, 30, 28), 5, False, False),
+    (4, (32, 24, 20), 5, False, 'flat_top'),
+    (4, (24, 20, 22), 5, False, 'huge'),
+    (8, (40, 24, 20), 5, False, False),
+    (8, (32, 20, 18), 4, True, True),
 ])
 def test_distributed_matches_whole_volume(tmp_path, world, shape, cell, ignore, big):
     mp.spawn(_worker, args=(world, _free_port(), shape, cell, str(tmp_path), ignore, big), nprocs=world, join=True)
@@ -87,7 +98,8 @@ def test_distributed_matches_whole_volume(tmp_path, world, shape, cell, ignore, 
         acc_n += len(ns[r])
         assert offs[r][1] == e_ref.shape[0] and offs[r][3] == nodes_ref.shape[0]
     # every shard is non-empty for these sizes (splitters balance the ranks)
-    assert all(len(x) > 0 for x in es)
+    if big != 'flat_top':
+        assert all(len(x) > 0 for x in es)
 
 
 def test_weighted_splitters_balance():
@@ -123,3 +135,36 @@ def test_split_counts_and_rows_roundtrip():
     assert rows.shape == (n, cdist.ROW_WORDS)
     k2, s2, r2 = cdist.unpack_rows(rows)
     assert torch.equal(k2, keys) and torch.equal(s2, sums) and torch.equal(r2, recs)
+
+
+def test_slab_halo_checked_against_offsets():
+    """dist.py refuses affinity offsets that reach past the slab's halo
+    instead of silently dropping the samples whose partner lies below it."""
+    lr = synthetic.LR_OFFSETS
+    cdist.check_slab_halo((40, 8, 8), lr, (27, 0, 0), None)        # enough halo planes
+    cdist.check_slab_halo((40, 8, 8), lr, (0, 0, 0), None)         # bottom slab: no neighbour below
+    cdist.check_slab_halo((40, 8, 8), None, (1, 0, 0), None)       # boundary maps: 1 plane
+    cdist.check_slab_halo((40, 8, 8), synthetic.NN_OFFSETS, (1, 0, 0), None)
+    with pytest.raises(ValueError, match='halo'):
+        cdist.check_slab_halo((40, 8, 8), lr, (1, 0, 0), None)
+    with pytest.raises(ValueError, match='upper halo'):
+        cdist.check_slab_halo((40, 8, 8), [[2, 0, 0]], (1, 0, 0), None)
+
+
+def test_device_splitters_match_numpy_restatement():
+    rng = np.random.default_rng(5)
+    for world in (2, 4, 8):
+        counts = rng.integers(0, 5000, world)
+        counts[rng.integers(0, world)] = 0
+        S = 32
+        samples = np.sort(rng.integers(-2 ** 62, 2 ** 62, (world, S)), axis=1)
+        sp = cdist.weighted_splitters(samples, counts, world)
+        # restatement: weighted quantiles of the kept samples
+        w = np.repeat(counts / S, S)
+        v = samples.reshape(-1)
+        v, w = v[w > 0], w[w > 0]
+        o = np.argsort(v, kind='stable')
+        v, w = v[o], w[o]
+        cw = np.cumsum(w)
+        idx = np.minimum(np.searchsorted(cw, cw[-1] * np.arange(1, world) / world, side='left'), v.size - 1)
+        np.testing.assert_array_equal(sp, v[idx])

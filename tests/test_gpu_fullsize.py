@@ -10,19 +10,24 @@ enumerated with torch comparisons, and torch.unique / scatter reductions give
 the edge set, the per-edge sample counts, sums, sums of squares, min and max.
 
 Bars: edges and counts bit-exact, nodes bit-exact, mean / var / min / max
-within 1e-5 relative (north_star), quantiles ordered and within [min, max]
-(their histogram is pinned by the oracle tests at small sizes).
+within 1e-5 relative (north_star).  Quantiles: for a random sample of ~20 k
+edges per configuration the exact per-edge 42-slot vigra histogram is rebuilt
+from the enumerated samples (torch bincount over (edge, slot)) and the
+oracle's vigra_quantiles (oracle/rag_oracle.py, SURVEY A.3) evaluated on it;
+the HIP quantile columns must match to 1e-9 (the bar is one bin, 1/40).
 """
 import numpy as np
 import pytest
 
 from cluster_tools_amd import rag
 from cluster_tools_amd import synthetic as S
+from oracle import rag_oracle as O
 
 pytestmark = pytest.mark.gpu
 torch = pytest.importorskip('torch')
 
 RTOL = 1e-5
+N_QSAMPLE = 20000
 
 
 def _faces(lab, data, axis):
@@ -39,7 +44,40 @@ def _faces(lab, data, axis):
     return u * (1 << 32) + v, da, db
 
 
-def _reference_boundary(lab, bnd):
+def _slots(x, lo=0.0, hi=1.0, nbins=40):
+    """vigra RangeHistogramBase binning of float64 samples -> slot in [0, 42)
+    (the oracle's histogram_slots in torch)."""
+    m = (nbins / (hi - lo)) * (x - lo)
+    idx = torch.trunc(m)
+    idx = torch.where(m == float(nbins), torch.full_like(idx, nbins - 1), idx)
+    slot = (idx + 1).clamp(0, nbins + 1)
+    slot = torch.where(idx < 0, torch.zeros_like(slot), slot)
+    return slot.to(torch.int64)
+
+
+def _check_quantiles(f, inv, x, seed=0, nbins=40):
+    """Exact per-edge histograms of a random edge sample, vigra quantiles of
+    the oracle on them, against the HIP quantile columns."""
+    E = f.shape[0]
+    g = torch.Generator(device='cpu').manual_seed(seed)
+    pick = torch.randperm(E, generator=g)[:min(N_QSAMPLE, E)].to(inv.device)
+    where = torch.full((E,), -1, dtype=torch.int64, device=inv.device)
+    where[pick] = torch.arange(pick.shape[0], device=inv.device)
+    sel = where[inv]
+    m = sel >= 0
+    h = torch.bincount(sel[m] * (nbins + 2) + _slots(x[m]), minlength=pick.shape[0] * (nbins + 2))
+    h = h.reshape(-1, nbins + 2).cpu().numpy()
+    fs = f[pick].cpu().numpy()
+    assert np.array_equal(h.sum(axis=1), fs[:, 9].astype(np.int64))          # histograms hold every sample
+    worst = 0.0
+    for i in range(fs.shape[0]):
+        q = O.vigra_quantiles(h[i], fs[i, 2], fs[i, 8], fs[i, 9], 0.0, 1.0)
+        worst = max(worst, float(np.abs(q[1:6] - fs[i, 3:8]).max()))
+    assert worst <= 1e-9, worst
+    return worst
+
+
+def _reference_boundary(lab, bnd, with_samples=False):
     keys, sa, sb = [], [], []
     for ax in range(3):
         k, a, b = _faces(lab, bnd, ax)
@@ -48,8 +86,11 @@ def _reference_boundary(lab, bnd):
         sb.append(b)
     keys = torch.cat(keys)
     x = torch.cat([torch.cat(sa), torch.cat(sb)]).double()
+    del sa, sb
     uk, inv, cnt = torch.unique(keys, return_inverse=True, return_counts=True)
+    del keys
     inv2 = torch.cat([inv, inv])
+    del inv
     E = uk.shape[0]
     s = torch.zeros(E, dtype=torch.float64, device=lab.device).scatter_add_(0, inv2, x)
     q = torch.zeros(E, dtype=torch.float64, device=lab.device).scatter_add_(0, inv2, x * x)
@@ -57,6 +98,8 @@ def _reference_boundary(lab, bnd):
         0, inv2, x, 'amin')
     mx = torch.full((E,), float('-inf'), dtype=torch.float64, device=lab.device).scatter_reduce_(
         0, inv2, x, 'amax')
+    if with_samples:
+        return (uk, 2 * cnt, s, q, mn, mx), (inv2, x)
     return uk, 2 * cnt, s, q, mn, mx
 
 
@@ -80,30 +123,36 @@ def test_configs1_512_boundary_full_size():
     """BASELINE configs[1]: 512^3 cell-10 supervoxels + boundary map."""
     lab, bnd = rag.synth_volume((512, 512, 512), cell=10, seed=0)
     res = rag.rag_features_handle(lab, bnd)
-    ref = _reference_boundary(lab, bnd)
+    ref, (inv, x) = _reference_boundary(lab, bnd, with_samples=True)
     _check(res, *ref)
+    _check_quantiles(res.features_torch(), inv, x, seed=1)
     nodes = res.nodes_torch()
     assert torch.equal(nodes, torch.unique(lab))
     assert ref[0].shape[0] > 900_000                                      # ~1e6 edges
     res.free()
 
 
-def test_configs4_fragmented_quarter_volume():
-    """BASELINE configs[4] density (cell 5) on a 256x512x1024 quarter volume:
-    many edges per tile, frequent table flushes, no direct-record overflow."""
-    lab, bnd = rag.synth_volume((256, 512, 1024), cell=5, seed=3)
+def test_configs4_fragmented_full_size():
+    """BASELINE configs[4]: 1024^3 at cell 5 (~6e7 edges): many edges per
+    tile, frequent table flushes, no direct-record overflow."""
+    lab, bnd = rag.synth_volume((1024, 1024, 1024), cell=5, seed=3)
     res = rag.rag_features_handle(lab, bnd)
-    _check(res, *_reference_boundary(lab, bnd))
+    ref, (inv, x) = _reference_boundary(lab, bnd, with_samples=True)
+    del lab, bnd
+    _check(res, *ref)
+    assert ref[0].shape[0] > 40_000_000
+    del ref
+    _check_quantiles(res.features_torch(), inv, x, seed=4)
     n_rec, n_direct = res.info()
     assert n_direct * 100 < n_rec                                         # the table path carries the load
     res.free()
 
 
 def test_configs3_long_range_affinities_edge_filter():
-    """BASELINE configs[3] offsets (12 long-range channels) at 192^3: a sample
+    """BASELINE configs[3] offsets (12 long-range channels) at 512^3: a sample
     aff[c,p] counts iff L[p] != L[p+o_c] and (min,max) is an edge of the
     nearest-neighbour RAG."""
-    shape = (192, 192, 192)
+    shape = (512, 512, 512)
     lab, bnd = rag.synth_volume(shape, cell=10, seed=5)
     affs = rag.synth_affinities(bnd, S.LR_OFFSETS)
     res = rag.rag_features_handle(lab, affs, offsets=S.LR_OFFSETS)
@@ -133,4 +182,106 @@ def test_configs3_long_range_affinities_edge_filter():
     mn = torch.full((E,), float('inf'), dtype=torch.float64, device=lab.device).scatter_reduce_(0, inv, x, 'amin')
     mx = torch.full((E,), float('-inf'), dtype=torch.float64, device=lab.device).scatter_reduce_(0, inv, x, 'amax')
     _check(res, uk, cnt, s, q, mn, mx)
+    _check_quantiles(res.features_torch(), inv, x, seed=3)
     res.free()
+
+
+# ---------------------------------------------------------------- configs[2]: 2048^3
+Z2 = 2048
+
+
+def _boundary_faces_chunked(lab, chunk=64):
+    """Number of boundary faces (L[p] != L[p + e_a]) of a resident volume,
+    counted per axis in z-chunks (torch, independent of the product path)."""
+    Z = lab.shape[0]
+    total = 0
+    for z0 in range(0, Z, chunk):
+        z1 = min(Z, z0 + chunk)
+        sl = lab[z0:z1]
+        total += int((sl[:, :, 1:] != sl[:, :, :-1]).sum().item())
+        total += int((sl[:, 1:, :] != sl[:, :-1, :]).sum().item())
+        z2 = min(Z, z1 + 1)
+        if z2 - 1 > z0:
+            total += int((lab[z0 + 1:z2] != lab[z0:z2 - 1]).sum().item())
+    return total
+
+
+def test_configs2_2048_full_size_properties():
+    """BASELINE configs[2] volume (2048^3, cell 16, 103 GB resident) on one
+    GPU.  The oracle cannot run at this size; size-independent properties:
+    sum of counts = 2 x the boundary faces counted per axis in torch, strictly
+    increasing (u < v) keys, nodes = union of the node lists of 8 z-slabs (each
+    with its halo plane), min <= mean <= max and min <= q10 <= ... <= max."""
+    lab, bnd = rag.synth_volume((Z2, Z2, Z2), cell=16, seed=0)
+    res = rag.rag_features_handle(lab, bnd)
+    e = res.edges_torch_i64()
+    f = res.features_torch()
+    assert e.shape[0] > 10_000_000
+    assert float(f[:, 9].sum().item()) == 2.0 * _boundary_faces_chunked(lab)
+    assert bool((e[:, 0] < e[:, 1]).all())
+    k = e[:, 0] * (1 << 32) + e[:, 1]
+    assert bool((k[1:] > k[:-1]).all())
+    del k
+    assert bool((f[:, 0] >= f[:, 2]).all()) and bool((f[:, 0] <= f[:, 8]).all())
+    qs = f[:, 2:9]
+    assert bool((qs[:, 1:] >= qs[:, :-1] - 1e-12).all())
+    nodes = res.nodes_torch()
+    res.free()
+    del e, f, qs
+    parts = []
+    for z0 in range(0, Z2, Z2 // 8):
+        h = 1 if z0 else 0
+        r = rag.rag_features_handle(lab[z0 - h:z0 + Z2 // 8], None, own_begin=(h, 0, 0))
+        parts.append(r.nodes_torch())
+        r.free()
+    assert torch.equal(nodes, torch.unique(torch.cat(parts)))
+
+
+def _slab_rank(rank, world, port, outdir):
+    import os
+    import torch.distributed as dist
+    from cluster_tools_amd import dist as cdist
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    torch.cuda.set_device(0)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    zr = Z2 // world
+    h = 1 if rank else 0
+    lab, bnd = rag.synth_volume((zr + h, Z2, Z2), cell=16, seed=0, z_offset=rank * zr - h,
+                                global_shape=(Z2, Z2, Z2))
+    res = cdist.rag_features_distributed(lab, bnd, own_begin=(h, 0, 0))
+    np.save(os.path.join(outdir, 'e%d.npy' % rank), res.edges())
+    np.save(os.path.join(outdir, 'f%d.npy' % rank), res.features())
+    np.save(os.path.join(outdir, 'o%d.npy' % rank), np.array([res.edge_offset, res.n_edges_global]))
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(400)
+def test_configs2_2048_two_rank_slabs_equal_single_call(tmp_path):
+    """BASELINE configs[2] z-slab sharding at full size: two ranks on the one
+    GPU (51.6 GB slab + halo plane each, exchange over gloo), shards
+    concatenated = the single-call result, edges bit-exact and features equal
+    (the merge of the boundary-crossing edges adds the same histograms; sums
+    may differ in the last bits)."""
+    import socket
+    import torch.multiprocessing as mp
+    lab, bnd = rag.synth_volume((Z2, Z2, Z2), cell=16, seed=0)
+    res = rag.rag_features_handle(lab, bnd)
+    e_ref, f_ref = res.edges(), res.features()
+    res.free()
+    del lab, bnd
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    rag.trim_cache()
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    port = s.getsockname()[1]
+    s.close()
+    mp.spawn(_slab_rank, args=(2, port, str(tmp_path)), nprocs=2, join=True)
+    e = np.concatenate([np.load(tmp_path / ('e%d.npy' % r)) for r in range(2)])
+    f = np.concatenate([np.load(tmp_path / ('f%d.npy' % r)) for r in range(2)])
+    o = [np.load(tmp_path / ('o%d.npy' % r)) for r in range(2)]
+    assert o[0][0] == 0 and o[1][0] == np.load(tmp_path / 'e0.npy').shape[0] and o[1][1] == e_ref.shape[0]
+    np.testing.assert_array_equal(e, e_ref)
+    np.testing.assert_array_equal(f[:, [2, 8, 9]], f_ref[:, [2, 8, 9]])
+    np.testing.assert_allclose(f, f_ref, rtol=1e-12, atol=1e-15)

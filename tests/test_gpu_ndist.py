@@ -215,3 +215,113 @@ def test_serialize_merged_graph(gpu, tmp_path, serialize_edges):
             np.testing.assert_array_equal(got, ref)
             rows = np.array([np.flatnonzero((new_uv == r).all(axis=1))[0] for r in ref], dtype=np.uint64)
             np.testing.assert_array_equal(g['edge_ids'].read_chunk(pos), rows)
+
+
+def test_merge_subgraphs_next_scale_varlen(gpu, tmp_path):
+    """n_scales=2: MergeSubGraphs at scale 1 (merge_sub_graphs.py:140-152,
+    184-193) unites the 2x2x2 scale-0 blocks of every 2x block into one varlen
+    chunk of s1/sub_graphs at that block's grid position.  The ids come in a
+    shuffled order (the chunk position must not depend on it)."""
+    lab, _ = S.generate(SHAPE, cell=5, seed=35, with_boundary=False)
+    p = _setup(tmp_path, lab)
+    blk, ids = _graph(p, False)
+    bs1 = [2 * b for b in BLOCK]
+    blk1 = blocking([0, 0, 0], list(SHAPE), bs1)
+    with n5.File(p) as f:
+        for k in ('nodes', 'edges'):   # merge_sub_graphs.py:42-50
+            f.require_dataset('s1/sub_graphs/' + k, shape=SHAPE, chunks=bs1, compression='gzip', dtype='uint64')
+    rng = np.random.default_rng(3)
+    for b1 in range(blk1.numberOfBlocks):
+        nb = blk1.getBlock(b1)
+        old = blk.getBlockIdsInBoundingBox(roiBegin=nb.begin, roiEnd=nb.end, blockHalo=[0, 0, 0]).tolist()
+        rng.shuffle(old)
+        ndist.mergeSubgraphs(p, subgraphKey='s0/sub_graphs', blockIds=old, outKey='s1/sub_graphs',
+                             serializeToVarlen=True)
+    with n5.File(p, 'r') as f:
+        g1 = f['s1/sub_graphs']
+        for b1 in range(blk1.numberOfBlocks):
+            nb = blk1.getBlock(b1)
+            pos = blk1.blockGridPosition(b1)
+            inner = tuple(slice(x, y) for x, y in zip(nb.begin, nb.end))
+            np.testing.assert_array_equal(g1['nodes'].read_chunk(pos), np.unique(lab[inner]))
+            # union of the scale-0 block sub-graphs = RAG faces with both voxels
+            # in some old block's halo'd box
+            parts = []
+            for ob in blk.getBlockIdsInBoundingBox(nb.begin, nb.end).tolist():
+                bb = blk.getBlock(int(ob))
+                outer = tuple(slice(max(x - 1, 0), y) for x, y in zip(bb.begin, bb.end))
+                e = O.rag_edges(lab[outer])
+                if e.shape[0]:
+                    parts.append(e)
+            got = g1['edges'].read_chunk(pos)
+            if not parts:
+                assert got is None
+                continue
+            ref = np.unique(np.concatenate(parts), axis=0)
+            np.testing.assert_array_equal(got.reshape(-1, 2), ref)
+
+
+def test_merge_feature_blocks_reference_layout(gpu, tmp_path):
+    """mergeFeatureBlocks on reference-layout sub_features (10 float64 columns,
+    no statistics companion - what nifty writes): count / mean / pooled
+    variance / min / max exact against the whole volume, quantiles exact for
+    edges held by one block and count-weighted (within [min, max]) otherwise."""
+    import shutil
+    lab, bnd = S.generate(SHAPE, cell=5, seed=36)
+    p = _setup(tmp_path, lab, bnd)
+    blk, ids = _graph(p, False)
+    E = ndist.Graph(p, 'graph').numberOfEdges
+    exact = _features(p, ids, E, ndist.extractBlockFeaturesFromBoundaryMaps_float32, increaseRoi=True)
+    shutil.rmtree(str(tmp_path / 'data.n5' / 's0' / 'sub_features_stats'))
+    with n5.File(p) as f:
+        f['features'][:] = np.zeros((E, 10))
+    for b, e in ((0, E // 3), (E // 3, E)):
+        ndist.mergeFeatureBlocks(p, 's0/sub_graphs', p, 's0/sub_features', p, 'features', blockIds=ids,
+                                 edgeIdBegin=b, edgeIdEnd=e, numberOfThreads=2)
+    with n5.File(p, 'r') as f:
+        compat = f['features'][:]
+        # edges with samples in exactly one block
+        owners = np.zeros(E, np.int64)
+        g = f['s0/sub_graphs']
+        for b in ids:
+            pos = blk.blockGridPosition(b)
+            eid = g['edge_ids'].read_chunk(pos)
+            rows = f['s0/sub_features'].read_chunk(pos)
+            if eid is None:
+                continue
+            rows = rows.reshape(-1, 10)
+            owners[eid[rows[:, 9] > 0].astype(np.int64)] += 1
+    np.testing.assert_array_equal(compat[:, 9], exact[:, 9])
+    np.testing.assert_allclose(compat[:, [0, 1]], exact[:, [0, 1]], rtol=1e-9, atol=1e-12)
+    np.testing.assert_array_equal(compat[:, [2, 8]], exact[:, [2, 8]])
+    one = owners == 1
+    assert one.any() and (owners > 1).any()
+    np.testing.assert_array_equal(compat[one, 3:8], exact[one, 3:8])
+    assert np.all(compat[:, 3:8] >= compat[:, 2:3] - 1e-12) and np.all(compat[:, 3:8] <= compat[:, 8:9] + 1e-12)
+
+
+def test_zarr_input_container(gpu, tmp_path):
+    """Input labels in a zarr container (graph_workflow.py:17-20), sub-graphs
+    in N5: the per-block graph equals the one from an N5 input."""
+    lab, _ = S.generate(SHAPE, cell=5, seed=37, with_boundary=False)
+    pz = str(tmp_path / 'in.zarr')
+    with n5.file_reader(pz) as f:
+        f.create_dataset('seg', data=lab, chunks=BLOCK, compression='gzip')
+    pg = _setup(tmp_path, lab)
+    blk = blocking([0, 0, 0], list(SHAPE), list(BLOCK))
+    for b in range(blk.numberOfBlocks):
+        bb = blk.getBlock(b)
+        ndist.computeMergeableRegionGraph(pz, 'seg', bb.begin, bb.end, pg, 's0/sub_graphs', False,
+                                          increaseRoi=True, serializeToVarlen=True)
+    with n5.File(pg, 'r') as f:
+        g = f['s0/sub_graphs']
+        for b in range(blk.numberOfBlocks):
+            bb = blk.getBlock(b)
+            pos = blk.blockGridPosition(b)
+            outer = tuple(slice(max(x - 1, 0), y) for x, y in zip(bb.begin, bb.end))
+            ref = O.rag_edges(lab[outer])
+            got = g['edges'].read_chunk(pos)
+            if ref.shape[0] == 0:
+                assert got is None
+            else:
+                np.testing.assert_array_equal(got.reshape(-1, 2), ref)

@@ -1,6 +1,7 @@
 """Host-side pieces of the drop-in (CPU only): the N5 codec,
 the nifty.tools.blocking mirror, blocks_in_volume, the synthetic generator."""
 import gzip
+import os
 import json
 import struct
 import zlib
@@ -181,3 +182,103 @@ def test_bench_cpu_baseline_chunks_cover_the_slab():
     u = np.unique(np.concatenate(parts), axis=0)
     np.testing.assert_array_equal(u, whole)
     assert '3 z-chunks on 3 worker processes' in info['sample']
+
+
+# ---------------------------------------------------------------- zarr, Graph forms, companion layout
+@pytest.mark.parametrize('codec', ['gzip', 'raw'])
+def test_zarr_roundtrip_and_layout(tmp_path, codec):
+    """zarr v2 input containers (graph_workflow.py:17-20 accepts zr / zarr):
+    C-order metadata, 'i.j.k' chunk keys, edge chunks stored at full shape."""
+    p = str(tmp_path / 'c.zarr')
+    data = (np.arange(5 * 7 * 9, dtype=np.uint64).reshape(5, 7, 9) * 7) % 1000
+    with n5.file_reader(p) as f:
+        ds = f.create_dataset('vol/seg', data=data, chunks=(2, 4, 4), compression=codec)
+        ds.attrs['resolution'] = [1, 2, 3]
+    root = tmp_path / 'c.zarr'
+    assert json.loads((root / '.zgroup').read_text())['zarr_format'] == 2
+    assert json.loads((root / 'vol' / '.zgroup').read_text())['zarr_format'] == 2
+    meta = json.loads((root / 'vol' / 'seg' / '.zarray').read_text())
+    assert meta['shape'] == [5, 7, 9] and meta['chunks'] == [2, 4, 4] and meta['dtype'] == '<u8'
+    assert json.loads((root / 'vol' / 'seg' / '.zattrs').read_text()) == {'resolution': [1, 2, 3]}
+    raw = (root / 'vol' / 'seg' / '2.1.2').read_bytes()         # last chunk in every axis
+    if codec == 'gzip':
+        raw = gzip.decompress(raw)
+    full = np.frombuffer(raw, '<u8').reshape(2, 4, 4)
+    np.testing.assert_array_equal(full[:1, :3, :1], data[4:5, 4:7, 8:9])
+    with n5.file_reader(p, 'r') as f:
+        ds = f['vol/seg']
+        np.testing.assert_array_equal(ds[:], data)
+        np.testing.assert_array_equal(ds[1:4, 2:7, 3:8], data[1:4, 2:7, 3:8])
+        assert ds.attrs['resolution'] == [1, 2, 3]
+    assert not os.path.exists(str(root / 'attributes.json'))
+
+
+def test_zarr_blosc_raises_and_other_formats_rejected(tmp_path):
+    p = tmp_path / 'b.zarr' / 'x'
+    p.mkdir(parents=True)
+    (tmp_path / 'b.zarr' / '.zgroup').write_text('{"zarr_format": 2}')
+    (p / '.zarray').write_text(json.dumps({'zarr_format': 2, 'shape': [4], 'chunks': [4], 'dtype': '<u8',
+                                           'compressor': {'id': 'blosc', 'cname': 'lz4'}, 'fill_value': 0,
+                                           'order': 'C', 'filters': None}))
+    (p / '0').write_bytes(b'\x00' * 8)
+    with n5.file_reader(str(tmp_path / 'b.zarr'), 'r') as f:
+        with pytest.raises(ValueError, match='blosc'):
+            f['x'][:]
+        assert (f['x'].read_chunk((1,)) is None)
+    with pytest.raises(ValueError):
+        n5.file_reader(str(tmp_path / 'a.h5'))
+
+
+def test_graph_constructor_forms(tmp_path):
+    """ndist.Graph(path, key), Graph(path_with_key) (ilastik/carving.py:28),
+    Graph(path_with_key, n_threads) (edges_from_skeletons.py:146), keyword
+    numberOfThreads (solve_subproblems.py:250); numberOfNodes semantics."""
+    from cluster_tools_amd import ndist
+    p = str(tmp_path / 'problem.n5')
+    nodes = np.array([0, 1, 2, 3, 4, 5], dtype=np.uint64)
+    uv = np.array([[0, 1], [1, 2], [2, 5], [3, 4]], dtype=np.uint64)
+    with n5.File(p) as f:
+        g = f.require_group('s0/graph')
+        g.create_dataset('nodes', data=nodes, chunks=(4,))
+        g.create_dataset('edges', data=uv, chunks=(3, 2))
+    forms = [ndist.Graph(p, 's0/graph'), ndist.Graph(p, 's0/graph', numberOfThreads=3),
+             ndist.Graph(os.path.join(p, 's0/graph')), ndist.Graph(os.path.join(p, 's0', 'graph'), 4),
+             ndist.Graph(os.path.join(p, 's0', 'graph'), numberOfThreads=2)]
+    for gr in forms:
+        np.testing.assert_array_equal(gr.uvIds(), uv)
+        np.testing.assert_array_equal(gr.nodes(), nodes)
+        # test_graph.py:113 literally: dense 0..max labels -> numberOfNodes == seg.max() + 1
+        assert gr.numberOfNodes == int(nodes.max()) + 1
+        assert gr.numberOfEdges == 4 and gr.maxNodeId == 5 and gr.maxEdgeId == 3
+    # non-dense labels: numberOfNodes counts distinct nodes (test_graph.py:78-80
+    # "number of nodes in nifty can be larger" for gridRag's max+1)
+    sparse = ndist.Graph(np.array([[2, 7], [7, 40]], dtype=np.uint64))
+    assert sparse.numberOfNodes == 3 and sparse.maxNodeId == 40
+    with pytest.raises(ValueError):
+        ndist.Graph(str(tmp_path / 'not_a_container' / 'graph'))
+    with pytest.raises(TypeError):
+        ndist.Graph()
+
+
+def test_stats_companion_words_roundtrip():
+    from cluster_tools_amd import ndist
+    rng = np.random.default_rng(1)
+    sums = rng.random((7, 2))
+    recs = rng.integers(0, 2 ** 32, (7, 48), dtype=np.uint64).astype(np.uint32)
+    w = ndist.encode_stats_words(sums, recs)
+    assert w.dtype == np.uint32 and w.shape == (7, 52) and w.nbytes == 7 * 208
+    s2, r2 = ndist.decode_stats_words(w.ravel())
+    np.testing.assert_array_equal(s2, sums)
+    np.testing.assert_array_equal(r2, recs)
+
+
+def test_blocks_in_volume_block_list_path(tmp_path):
+    lp = tmp_path / 'blocks.json'
+    lp.write_text(json.dumps([1, 9, 11, 12]))
+    assert B.blocks_in_volume((10, 9, 7), (4, 4, 4), block_list_path=str(lp)) == [1, 9, 11, 12]
+    ids = B.blocks_in_volume((10, 9, 7), (4, 4, 4), [4, 4, 4], [None, None, None], block_list_path=str(lp))
+    assert ids == [9, 11]
+    ids, blk = B.blocks_in_volume((10, 9, 7), (4, 4, 4), return_blocking=True)
+    assert blk.numberOfBlocks == 18 and ids == list(range(18))
+    with pytest.raises(AssertionError):
+        B.blocks_in_volume((10, 9, 7), (4, 4, 4), block_list_path=str(tmp_path / 'missing.json'))

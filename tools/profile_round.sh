@@ -16,4 +16,4 @@ timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_wri
     python tools/prof_scan.py boundary > $O/pmc_write.log 2>&1 && echo WRITE_OK &&
 CTG_ABLATE=8 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_fetch_loads -o run -- \
     python tools/prof_scan.py boundary > $O/pmc_fetch_loads.log 2>&1 && echo FETCH_LOADS_OK &&
-timeout -k 10 240 python tools_ablate.py > $O/ablate.jsonl 2> $O/ablate.err && echo ABLATE_OK
+timeout -k 10 240 python tools/ablate2.py > $O/ablate.jsonl 2> $O/ablate.err && echo ABLATE_OK
