@@ -7,7 +7,7 @@ TAG=${1:-r2a}
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 O=gpurun_out/$TAG
 mkdir -p $O
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 150 --timeout-method thread > $O/pytest_gpu.log 2>&1; echo "PYTEST rc=$?"
+timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 150 --timeout-method thread > $O/pytest_gpu.log 2>&1; rc=$?; echo "PYTEST rc=$rc"; [ $rc -le 1 ] &&
 timeout -k 10 200 python bench.py --steps 20 --warmup 3 --no-cpu-baseline > $O/bench.json 2> $O/bench.err && echo BENCH_OK && cat $O/bench.json &&
 CTG_PROF_SIZE=1024 timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $O/lr_trace -o run -- \
     python tools/prof_scan.py lr > $O/lr_trace.log 2>&1 && echo LR_TRACE_OK &&
