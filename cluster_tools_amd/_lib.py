@@ -25,6 +25,11 @@ CTG_MAX_CHANNELS = 24
 CTG_N_FEATURES = 10
 CTG_NBINS = 40
 CTG_WIDE_RECORD_WORDS = 48
+CTG_IO_N5 = 0
+CTG_IO_ZARR_DOT = 1
+CTG_IO_ZARR_SLASH = 2
+CTG_IO_RAW = 0
+CTG_IO_GZIP = 1
 
 _lock = threading.Lock()
 _lib = None
@@ -67,6 +72,14 @@ PROTOTYPES = {
                                         ctypes.c_uint64, ctypes.c_double, c_vp]),
     'ctg_synth_affinities': (ctypes.c_int, [c_vp, c_vp, c_vp, ctypes.c_int, c_vp, c_vp]),
     'ctg_trim': (ctypes.c_int, []),
+    'ctg_io_read_box': (ctypes.c_int, [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                       c_vp, c_vp, ctypes.c_int, c_vp, c_vp, c_vp, ctypes.c_int]),
+    'ctg_io_read_varlen': (ctypes.c_int, [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.c_int64, c_vp,
+                                          ctypes.c_int, c_vp, c_vp, ctypes.c_int]),
+    'ctg_io_free': (None, [c_vp]),
+    'ctg_io_write_chunks': (ctypes.c_int, [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                           ctypes.c_int64, c_vp, c_vp, c_vp, c_vp, ctypes.c_int, ctypes.c_int,
+                                           ctypes.c_int, ctypes.c_int]),
     'ctg_set_profiling': (ctypes.c_int, [ctypes.c_int]),
     'ctg_last_timings': (ctypes.c_int, [c_dblp, ctypes.c_int]),
 }

@@ -397,9 +397,104 @@ __device__ __forceinline__ void fold_stats(Table& T, const StageT& e, int s, Rec
     }
 }
 
+#ifndef CTG_RUNCOMB
+#define CTG_RUNCOMB 0
+#endif
+// fold_stats with run combining (see CTG_RUNCOMB below): every lane of the
+// wave calls it (DPP needs the whole wave); `valid` marks real entries.
+template <int D>
+__device__ __forceinline__ uint32_t dpp_shr_u(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x110 + D, 0xf, 0xf, false);
+}
+template <int D>
+__device__ __forceinline__ double dpp_shr_d(double v) {
+    const uint64_t b = (uint64_t)__double_as_longlong(v);
+    const uint32_t lo = dpp_shr_u<D>((uint32_t)b), hi = dpp_shr_u<D>((uint32_t)(b >> 32));
+    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+
+template <int MODE, bool FAST40, typename StageT>
+__device__ __forceinline__ void fold_stats_runs(Table& T, const StageT& e, int s, bool valid, int lane, RecordBuf R,
+                                                Counters* C, double scale, double offset, int ablate) {
+    constexpr bool BND = MODE == MODE_BOUNDARY;
+    constexpr bool AFF = MODE == MODE_AFFINITY;
+    constexpr int G = CTG_RUNCOMB;
+    const bool adj = AFF && e.w == MARK_ADJ;
+    const float a = __uint_as_float(e.z);
+    const float b = BND ? __uint_as_float(e.w) : a;
+    const int sa = adj ? -1 : sample_slot<FAST40>(a, scale, offset);
+    const int sb = BND ? sample_slot<FAST40>(b, scale, offset) : -1;
+    const double da = (double)a, db = (double)b;
+    uint32_t n = (!valid || adj) ? 0u : (BND ? 2u : 1u);
+    double ds = n ? (BND ? da + db : da) : 0.0;
+    double dq = n ? (BND ? da * da + db * db : da * da) : 0.0;
+    uint32_t mn = n ? f2ord(fminf(a, b)) : ORD_POS_INF, mx = n ? f2ord(fmaxf(a, b)) : ORD_NEG_INF;
+    uint32_t fl = (valid && adj) ? ADJ_FLAG : 0u;
+    // run heads: group start, key change, invalid entry or a direct record
+    // (on either side) -- directs are emitted one face each
+    const int sk = valid ? s : -2;
+    const uint32_t px = dpp_shr_u<1>(e.x), py = dpp_shr_u<1>(e.y), ps = dpp_shr_u<1>((uint32_t)sk);
+    const bool head = (lane & (G - 1)) == 0 || px != e.x || py != e.y || (int)ps != sk || sk < 0;
+    const uint64_t hm = __ballot(head);
+    const uint64_t le = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);
+    const int hp = 63 - __clzll(hm & le);   // this lane's run head
+#pragma unroll
+    for (int d = 1; d < G; d <<= 1) {
+        uint32_t on, omn, omx, ofl;
+        double ods, odq;
+        if (d == 1) {
+            on = dpp_shr_u<1>(n); omn = dpp_shr_u<1>(mn); omx = dpp_shr_u<1>(mx); ofl = dpp_shr_u<1>(fl);
+            ods = dpp_shr_d<1>(ds); odq = dpp_shr_d<1>(dq);
+        } else if (d == 2) {
+            on = dpp_shr_u<2>(n); omn = dpp_shr_u<2>(mn); omx = dpp_shr_u<2>(mx); ofl = dpp_shr_u<2>(fl);
+            ods = dpp_shr_d<2>(ds); odq = dpp_shr_d<2>(dq);
+        } else {
+            on = dpp_shr_u<4>(n); omn = dpp_shr_u<4>(mn); omx = dpp_shr_u<4>(mx); ofl = dpp_shr_u<4>(fl);
+            ods = dpp_shr_d<4>(ds); odq = dpp_shr_d<4>(dq);
+        }
+        if (lane - d >= hp) {
+            n += on;
+            ds += ods;
+            dq += odq;
+            mn = min(mn, omn);
+            mx = max(mx, omx);
+            fl |= ofl;
+        }
+    }
+    if (!valid) return;
+    const bool tail = lane == 63 || ((lane + 1) & (G - 1)) == 0 || ((hm >> (lane + 1)) & 1ull);
+    const uint64_t key = ((uint64_t)e.x << 32) | e.y;
+    if (s < 0) {   // direct record: its own run of one face
+        emit_direct(R, C, key, n | fl, sa, sb, ds, dq, mn, mx, true);
+        return;
+    }
+    if (tail) {
+        if (fl) atomicOr(&T.w[s][21], ADJ_FLAG);
+        if (n) {
+            atomicAdd(&T.sum[s], ds);
+            atomicAdd(&T.sq[s], dq);
+            atomicMin(&T.w[s][22], mn);
+            atomicMax(&T.w[s][23], mx);
+            atomicAdd(&T.w[s][21], n);
+        }
+    }
+    if (adj || (ablate & 128)) return;
+    if constexpr (BND) hist_add2(T, s, sa, sb);
+    else atomicAdd(&T.w[s][sa >> 1], 1u << ((sa & 1) * 16));
+}
+
 // Fold the wave's nb staged entries into the LDS edge table: NPER entries per
 // lane (lane, lane+64, ...), their stage reads and home-bucket reads issued
 // together so the LDS round trips of the entries overlap.
+// Run combining (CTG_RUNCOMB = G > 0): consecutive stage entries are mostly
+// the same face key (a boundary patch along x, a long-range pair along x), and
+// their statistics atomics then all hit one LDS address and serialise.  Within
+// aligned groups of G lanes the contributions (count, sum, sum of squares,
+// min, max, ADJ) of equal-key neighbours are combined with a segmented DPP
+// scan, and only the last lane of each run issues the statistics atomics; the
+// histogram keeps one atomic per sample.
+constexpr int RUNCOMB = CTG_RUNCOMB;
+
 template <int MODE, bool FAST40, typename StageT, int NPER>
 __device__ __forceinline__ void fold_batch(Table& T, const StageT* __restrict__ stage, int nb, int lane, RecordBuf R,
                                            Counters* C, double scale, double offset, bool& need, int ablate) {
@@ -422,29 +517,36 @@ __device__ __forceinline__ void fold_batch(Table& T, const StageT* __restrict__ 
     }
 #pragma unroll
     for (int i = 0; i < NPER; ++i) {
-        if (lane + WAVE * i >= nb) continue;
-        const uint64_t key = ((uint64_t)e[i].x << 32) | e[i].y;
-        int empty;
-        int s = bucket_match(b01[i], b23[i], h[i], key, empty);
-        if (s < 0) {
-            // not in the home bucket: claim its first empty slot with one CAS
-            if (empty >= 0) {
-                const uint64_t old = atomicCAS((unsigned long long*)&T.key[h[i] + empty],
-                                               (unsigned long long)EMPTY_KEY, (unsigned long long)key);
-                if (old == EMPTY_KEY) {
-                    if (atomicAdd(&T.used, 1u) + 1u > FILL_SOFT) need = true;
-                    s = (int)h[i] + empty;
-                } else if (old == key) {
-                    s = (int)h[i] + empty;
+        const bool valid = lane + WAVE * i < nb;
+        int s = -1;
+        if (valid) {
+            const uint64_t key = ((uint64_t)e[i].x << 32) | e[i].y;
+            int empty;
+            s = bucket_match(b01[i], b23[i], h[i], key, empty);
+            if (s < 0) {
+                // not in the home bucket: claim its first empty slot with one CAS
+                if (empty >= 0) {
+                    const uint64_t old = atomicCAS((unsigned long long*)&T.key[h[i] + empty],
+                                                   (unsigned long long)EMPTY_KEY, (unsigned long long)key);
+                    if (old == EMPTY_KEY) {
+                        if (atomicAdd(&T.used, 1u) + 1u > FILL_SOFT) need = true;
+                        s = (int)h[i] + empty;
+                    } else if (old == key) {
+                        s = (int)h[i] + empty;
+                    }
+                }
+                if (s < 0) {
+                    s = table_insert(T, h[i], empty, key);
+                    need |= s < 0 || (s & INSERT_OVER) != 0;
+                    s = s < 0 ? s : (s & (INSERT_OVER - 1));
                 }
             }
-            if (s < 0) {
-                s = table_insert(T, h[i], empty, key);
-                need |= s < 0 || (s & INSERT_OVER) != 0;
-                s = s < 0 ? s : (s & (INSERT_OVER - 1));
-            }
         }
-        fold_stats<MODE, FAST40, StageT>(T, e[i], s, R, C, scale, offset, need, ablate);
+        if constexpr (RUNCOMB > 0 && MODE != MODE_GRAPH) {
+            fold_stats_runs<MODE, FAST40, StageT>(T, e[i], s, valid, lane, R, C, scale, offset, ablate);
+        } else {
+            if (valid) fold_stats<MODE, FAST40, StageT>(T, e[i], s, R, C, scale, offset, need, ablate);
+        }
     }
 }
 
@@ -714,7 +816,7 @@ __global__ __launch_bounds__(SCAN_THREADS, 4) void k_face_scan(ScanParams P, Rec
 #pragma unroll
                             for (int j = 0; j < CG; ++j) act[j] = act[j] && lq[j] != lc;
                             // long-range channels: only pairs that are RAG edges
-                            if (P.adj_set != nullptr && ((P.lr_mask >> c0) & ((1u << CG) - 1u))) {
+                            if (P.adj_set != nullptr && ((P.lr_mask >> c0) & ((1u << CG) - 1u)) && !(ablate & 512)) {
                                 uint64_t key[CG];
                                 unsigned long long k0[CG];
                                 bool lr[CG];

@@ -123,6 +123,36 @@ def _normalize_compression(compression):
     raise ValueError('unsupported compression %r' % (compression,))
 
 
+_NATIVE = None
+
+
+def _native():
+    """libctg.so's chunk codec (ctg_io_*), or None when the library is not
+    built (the pure-Python codec below is then used; it is also the reference
+    the native one is tested against)."""
+    global _NATIVE
+    if _NATIVE is None:
+        if os.environ.get('CTG_IO_PYTHON'):
+            _NATIVE = False
+        else:
+            try:
+                from . import _lib
+                _NATIVE = _lib.load()
+            except Exception:
+                _NATIVE = False
+    return _NATIVE or None
+
+
+def _io_threads(n_threads):
+    return max(1, int(n_threads) if n_threads and n_threads > 1 else min(16, os.cpu_count() or 1))
+
+
+def _i64(vals):
+    import ctypes
+    vals = [int(v) for v in vals]
+    return (ctypes.c_int64 * max(1, len(vals)))(*vals)
+
+
 def _decompress(buf):
     if len(buf) >= 2 and buf[0] == 0x1F and buf[1] == 0x8B:
         return zlib.decompress(buf, 16 + zlib.MAX_WBITS)
@@ -159,6 +189,95 @@ class Dataset:
 
     def chunk_exists(self, pos):
         return os.path.exists(self._chunk_path(pos))
+
+    # --- native fast paths (ctg_io_*) ------------------------------------
+    _FORMAT = 0        # CTG_IO_N5
+
+    def _big_endian(self):
+        return 1
+
+    def _ctype(self):
+        c = self.compression.get('type', 'raw')
+        return {'raw': 0, 'gzip': 1}.get(c)
+
+    def _level(self):
+        lv = self.compression.get('level', 5)
+        return 5 if lv is None or lv < 0 else int(lv)
+
+    def read_box_native(self, bb, n_threads=None):
+        """C-order box [(b, e), ...] through ctg_io_read_box, or None."""
+        lib = _native()
+        ct = self._ctype()
+        if lib is None or ct is None:
+            return None
+        import ctypes
+        out = np.empty(tuple(e - b for b, e in bb), dtype=self.dtype.newbyteorder('='))
+        rc = lib.ctg_io_read_box(self.path.encode(), self._FORMAT, self.dtype.itemsize, self._big_endian(),
+                                 self.ndim, _i64(self.shape), _i64(self.chunks), ct, _i64([b for b, _ in bb]),
+                                 _i64([e for _, e in bb]), out.ctypes.data_as(ctypes.c_void_p),
+                                 _io_threads(n_threads or self.n_threads))
+        if rc != 0:
+            msg = lib.ctg_last_error()
+            raise OSError(msg.decode() if msg else 'ctg_io_read_box failed')
+        return out
+
+    def write_chunks(self, positions, datas, varlen=False, n_threads=None):
+        """Write many chunks at once (native thread pool when available).
+        Default-mode chunks must have their grid cell's shape."""
+        positions = [tuple(int(p) for p in pos) for pos in positions]
+        datas = [np.ascontiguousarray(np.asarray(d, dtype=self.dtype)) for d in datas]
+        lib = _native()
+        ct = self._ctype()
+        if lib is None or ct is None or not positions:
+            for pos, d in zip(positions, datas):
+                self.write_chunk(pos, d, varlen)
+            return
+        import ctypes
+        nd = self.ndim
+        shapes = []
+        for pos, d in zip(positions, datas):
+            cs = self._chunk_shape(pos)
+            if not varlen and self._FORMAT == 0 and tuple(d.shape) != tuple(cs):
+                raise ValueError('chunk %s has shape %s, expected %s' % (pos, d.shape, cs))
+            shapes.append(cs)
+        n = len(positions)
+        ptrs = (ctypes.c_void_p * n)(*[d.ctypes.data for d in datas])
+        counts = _i64([d.size for d in datas])
+        rc = lib.ctg_io_write_chunks(self.path.encode(), self._FORMAT, self.dtype.itemsize, self._big_endian(), nd,
+                                     n, _i64([x for pos in positions for x in pos]),
+                                     _i64([x for cs in shapes for x in cs]), ptrs, counts, int(bool(varlen)), ct,
+                                     self._level(), _io_threads(n_threads or self.n_threads))
+        if rc != 0:
+            msg = lib.ctg_last_error()
+            raise OSError(msg.decode() if msg else 'ctg_io_write_chunks failed')
+
+    def read_chunks(self, positions, n_threads=None):
+        """Varlength chunks at many grid positions (None where missing)."""
+        positions = [tuple(int(p) for p in pos) for pos in positions]
+        lib = _native()
+        ct = self._ctype()
+        if lib is None or ct is None or self._FORMAT != 0 or not positions:
+            return [self.read_chunk(pos) for pos in positions]
+        import ctypes
+        n = len(positions)
+        outs = (ctypes.c_void_p * n)()
+        counts = (ctypes.c_int64 * n)()
+        rc = lib.ctg_io_read_varlen(self.path.encode(), self.dtype.itemsize, self.ndim, n,
+                                    _i64([x for pos in positions for x in pos]), ct, outs, counts,
+                                    _io_threads(n_threads or self.n_threads))
+        if rc != 0:
+            msg = lib.ctg_last_error()
+            raise OSError(msg.decode() if msg else 'ctg_io_read_varlen failed')
+        res = []
+        dt = self.dtype.newbyteorder('=')
+        for i in range(n):
+            if counts[i] < 0:
+                res.append(None)
+                continue
+            buf = (ctypes.c_char * (int(counts[i]) * dt.itemsize)).from_address(outs[i]) if counts[i] else b''
+            res.append(np.frombuffer(bytes(buf), dtype=dt).copy() if counts[i] else np.zeros(0, dt))
+            lib.ctg_io_free(outs[i])
+        return res
 
     def _encode(self, arr, varlen, shape):
         be = np.ascontiguousarray(arr).astype(self.dtype.newbyteorder('>'), copy=False).tobytes()
@@ -251,6 +370,9 @@ class Dataset:
 
     def __getitem__(self, index):
         bb, squeeze = self._norm_index(index)
+        nat = self.read_box_native(bb)
+        if nat is not None:
+            return nat.squeeze(axis=squeeze) if squeeze else nat
         out = np.full(tuple(e - b for b, e in bb), getattr(self, 'fill_value', 0), dtype=self.dtype)
 
         def one(pos):
@@ -278,6 +400,16 @@ class Dataset:
         bb, _ = self._norm_index(index)
         shape = tuple(e - b for b, e in bb)
         value = np.broadcast_to(np.asarray(value, dtype=self.dtype), shape)
+        aligned = all(b % c == 0 and (e % c == 0 or e == s) for (b, e), c, s in zip(bb, self.chunks, self.shape))
+        if aligned and _native() is not None and self._ctype() is not None and all(x > 0 for x in shape):
+            pos_list = [tuple(int(x) for x in p) for p in self._chunks_in(bb)]
+            datas = []
+            for pos in pos_list:
+                cs = self._chunk_shape(pos)
+                src = tuple(slice(p * c - b, p * c - b + n) for p, c, (b, _), n in zip(pos, self.chunks, bb, cs))
+                datas.append(value[src])
+            self.write_chunks(pos_list, datas)
+            return
 
         def one(pos):
             cb = [p * c for p, c in zip(pos, self.chunks)]
@@ -331,6 +463,34 @@ class ZarrArray(Dataset):
         self.sep = meta.get('dimension_separator', '.')
         self.attrs = Attributes(path, _ZATTRS)
         self.n_threads = 1
+
+    @property
+    def _FORMAT(self):  # noqa: N802
+        return 2 if self.sep == '/' else 1   # CTG_IO_ZARR_SLASH / CTG_IO_ZARR_DOT
+
+    def _big_endian(self):
+        return 1 if self.dtype.byteorder == '>' else 0
+
+    def _ctype(self):
+        c = self.compressor
+        if c is None:
+            return 0
+        return 1 if c.get('id') in _ZARR_CODECS else None   # other codecs: the Python path raises
+
+    def _level(self):
+        lv = (self.compressor or {}).get('level', 5)
+        return 5 if lv is None or lv < 0 else int(lv)
+
+    def write_chunks(self, positions, datas, varlen=False, n_threads=None):
+        if varlen:
+            raise ValueError('zarr has no varlength chunks (the sub-graph datasets are N5)')
+        full = []
+        for d in datas:
+            d = np.asarray(d, dtype=self.dtype)
+            f = np.full(self.chunks, self.fill_value, dtype=self.dtype)
+            f[tuple(slice(0, n) for n in d.shape)] = d
+            full.append(f)
+        Dataset.write_chunks(self, positions, full, False, n_threads)
 
     def _codec(self):
         c = self.compressor

@@ -153,6 +153,35 @@ int ctg_synth_volume(uint64_t* labels, float* boundary, const int64_t* shape,
 int ctg_synth_affinities(const float* boundary, float* affs, const int64_t* shape,
                          int n_channels, const int32_t* offsets, void* stream);
 
+/*
+ * Native N5 / zarr chunk I/O (host memory; zlib + a thread pool).  The ndist
+ * mirror reads the ROIs and writes the varlength chunks of the per-block path
+ * through these (z5's role in the reference: graph/initial_sub_graphs.py:72-75,
+ * features/block_edge_features.py:63-64, 236).
+ *   format       CTG_IO_N5 | CTG_IO_ZARR_DOT (i.j.k keys) | CTG_IO_ZARR_SLASH
+ *   big_endian   1: stored elements are big-endian (N5; zarr '>' dtypes)
+ *   compression  CTG_IO_RAW | CTG_IO_GZIP (gzip or zlib streams on read)
+ */
+#define CTG_IO_N5 0
+#define CTG_IO_ZARR_DOT 1
+#define CTG_IO_ZARR_SLASH 2
+#define CTG_IO_RAW 0
+#define CTG_IO_GZIP 1
+/* C-order box [begin, end) of a chunked dataset into `out` (missing chunks = 0) */
+int ctg_io_read_box(const char* ds_path, int format, int dtype_size, int big_endian, int ndim, const int64_t* shape,
+                    const int64_t* chunks, int compression, const int64_t* begin, const int64_t* end, void* out,
+                    int n_threads);
+/* varlength N5 chunks at n_chunks grid positions: out[i] = malloc'ed native-
+ * endian elements (free with ctg_io_free), n_out[i] = count, or NULL / -1 if
+ * the chunk does not exist */
+int ctg_io_read_varlen(const char* ds_path, int dtype_size, int ndim, int64_t n_chunks, const int64_t* positions,
+                       int compression, void** out, int64_t* n_out, int n_threads);
+void ctg_io_free(void* p);
+/* write n_chunks chunks (default mode with chunk_shapes, or N5 varlength) */
+int ctg_io_write_chunks(const char* ds_path, int format, int dtype_size, int big_endian, int ndim, int64_t n_chunks,
+                        const int64_t* positions, const int64_t* chunk_shapes, const void* const* data,
+                        const int64_t* n_elements, int varlen, int compression, int level, int n_threads);
+
 /* release every device block the library caches on the current device
  * (workspace and allocator pool); result handles stay valid */
 int ctg_trim(void);

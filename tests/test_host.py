@@ -282,3 +282,74 @@ def test_blocks_in_volume_block_list_path(tmp_path):
     assert blk.numberOfBlocks == 18 and ids == list(range(18))
     with pytest.raises(AssertionError):
         B.blocks_in_volume((10, 9, 7), (4, 4, 4), block_list_path=str(tmp_path / 'missing.json'))
+
+
+# ---------------------------------------------------------------- native chunk codec (ctg_io_*)
+def _with_codec(monkeypatch, native):
+    monkeypatch.setattr(n5, '_NATIVE', None)
+    if native:
+        monkeypatch.delenv('CTG_IO_PYTHON', raising=False)
+    else:
+        monkeypatch.setenv('CTG_IO_PYTHON', '1')
+
+
+@pytest.mark.parametrize('ext,comp,dtype', [('n5', 'gzip', 'uint64'), ('n5', 'raw', 'float32'),
+                                            ('n5', 'gzip', 'uint8'), ('zarr', 'gzip', 'uint64'),
+                                            ('zarr', 'raw', 'float32')])
+@pytest.mark.parametrize('writer', ['native', 'python'])
+def test_native_codec_matches_python(tmp_path, monkeypatch, ext, comp, dtype, writer):
+    """libctg.so's threaded chunk codec and the Python codec read each other's
+    chunks (edge chunks, missing chunks, boxes not aligned to chunks)."""
+    rng = np.random.default_rng(2)
+    data = rng.integers(0, 255, (19, 23, 30)).astype(dtype)
+    p = str(tmp_path / ('c.' + ext))
+    _with_codec(monkeypatch, writer == 'native')
+    assert (n5._native() is not None) == (writer == 'native')
+    with n5.file_reader(p) as f:
+        ds = f.create_dataset('d', shape=data.shape, chunks=(4, 8, 7), dtype=dtype, compression=comp)
+        ds[:16, :, :] = data[:16]          # chunk-aligned box: batched writer
+        ds[16:, :, :] = data[16:]          # unaligned box: read-modify-write
+        ds.n_threads = 3
+    for reader in ('native', 'python'):
+        _with_codec(monkeypatch, reader == 'native')
+        with n5.file_reader(p, 'r') as f:
+            ds = f['d']
+            np.testing.assert_array_equal(ds[:], data)
+            np.testing.assert_array_equal(ds[3:17, 5:21, 2:29], data[3:17, 5:21, 2:29])
+            np.testing.assert_array_equal(ds[7, 2:9, :], data[7, 2:9, :])
+    # a missing chunk reads as zeros
+    _with_codec(monkeypatch, True)
+    import shutil
+    if ext == 'n5':
+        os.remove(str(tmp_path / "c.n5" / "d" / "0" / "0" / "0"))     # chunk (0,0,0) = <x>/<y>/<z>
+    else:
+        os.remove(str(tmp_path / 'c.zarr' / 'd' / '0.0.0'))
+    with n5.file_reader(p, 'r') as f:
+        assert not f['d'][:4, :8, :7].any()
+        np.testing.assert_array_equal(f['d'][4:, :, :], data[4:])
+
+
+def test_native_varlen_batches(tmp_path, monkeypatch):
+    _with_codec(monkeypatch, True)
+    p = str(tmp_path / 'v.n5')
+    rng = np.random.default_rng(3)
+    with n5.File(p) as f:
+        ds = f.create_dataset('s', shape=(10, 10, 10), chunks=(5, 5, 5), dtype='uint64', compression='gzip')
+        pos = [(0, 0, 0), (1, 0, 1), (1, 1, 1), (0, 1, 0)]
+        vals = [rng.integers(0, 2 ** 63, n, dtype=np.uint64) for n in (0, 7, 1000, 3)]
+        ds.write_chunks(pos, vals, varlen=True, n_threads=4)
+        got = ds.read_chunks(pos + [(1, 1, 0)], n_threads=4)
+        assert got[-1] is None
+        for a, b in zip(got, vals):
+            np.testing.assert_array_equal(a, b)
+        # python reader on native-written varlen chunks and vice versa
+        _with_codec(monkeypatch, False)
+        for pp, v in zip(pos, vals):
+            np.testing.assert_array_equal(ds.read_chunk(pp), v)
+        ds.write_chunk((0, 0, 1), vals[2], True)
+        _with_codec(monkeypatch, True)
+        np.testing.assert_array_equal(ds.read_chunks([(0, 0, 1)])[0], vals[2])
+        # a default-mode chunk is not a varlength chunk
+        f.create_dataset('d', data=np.ones((4, 4, 4), np.uint64), chunks=(2, 2, 2))
+        with pytest.raises(OSError):
+            f['d'].read_chunks([(0, 0, 0)])
