@@ -50,6 +50,13 @@ PROTOTYPES = {
     'ctg_rag_features': (ctypes.c_int, [c_vp, ctypes.c_int, c_vp, ctypes.c_int, ctypes.c_int, c_vp,
                                         c_vp, c_vp, c_vp, ctypes.c_int, ctypes.c_double, ctypes.c_double,
                                         ctypes.c_int, ctypes.c_int, c_vp, ctypes.POINTER(c_vp)]),
+    'ctg_rag_blocks': (ctypes.c_int, [c_vp, ctypes.c_int, c_vp, ctypes.c_int, ctypes.c_int, c_vp, c_vp,
+                                      ctypes.c_int, ctypes.c_int64, ctypes.c_int64, ctypes.c_int, ctypes.c_double,
+                                      ctypes.c_double, ctypes.c_int, ctypes.c_int, c_vp, ctypes.POINTER(c_vp)]),
+    'ctg_result_num_blocks': (ctypes.c_int, [c_vp]),
+    'ctg_result_block_offsets': (ctypes.c_int, [c_vp, c_vp, c_vp]),
+    'ctg_host_alloc': (c_vp, [ctypes.c_int64]),
+    'ctg_host_free': (None, [c_vp]),
     'ctg_unique_labels': (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, ctypes.c_int, c_vp, ctypes.POINTER(c_vp)]),
     'ctg_merge_stats': (ctypes.c_int, [c_vp, c_vp, c_vp, ctypes.c_int64, ctypes.c_double, ctypes.c_double,
                                        ctypes.c_int, ctypes.c_int, c_vp, ctypes.POINTER(c_vp)]),
@@ -83,6 +90,13 @@ PROTOTYPES = {
     'ctg_set_profiling': (ctypes.c_int, [ctypes.c_int]),
     'ctg_last_timings': (ctypes.c_int, [c_dblp, ctypes.c_int]),
 }
+
+
+class BlockDesc(ctypes.Structure):
+    """ctg_block_desc (include/ctg.h)."""
+    _fields_ = [('label_offset', ctypes.c_int64), ('data_offset', ctypes.c_int64),
+                ('shape', ctypes.c_int64 * 3), ('own_begin', ctypes.c_int64 * 3), ('own_end', ctypes.c_int64 * 3),
+                ('graph_begin', ctypes.c_int64 * 3), ('graph_end', ctypes.c_int64 * 3)]
 
 
 class CtgError(RuntimeError):

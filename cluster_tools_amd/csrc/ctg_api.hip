@@ -27,9 +27,15 @@ hipError_t launch_pack_pairs(int64_t n, const uint64_t* uv, int nb, uint64_t* sk
 hipError_t launch_max_pairs(int64_t n, const uint64_t* uv, unsigned long long* out, hipStream_t s);
 hipError_t launch_reduce(int64_t E, const uint32_t* dE, const uint64_t* uniq, const uint32_t* runs,
                          const uint32_t* offs, const uint32_t* perm32, const uint64_t* perm64, int ib,
-                         const RecordBuf& R, int wide, int stats, int nb, int need_adj, int ignore_label, double scale,
-                         double offset, const ReduceOut& O,
-                         hipStream_t s);
+                         const RecordBuf& R, int wide, int stats, int nb, uint64_t umask, int need_adj,
+                         int ignore_label, double scale, double offset, const ReduceOut& O, hipStream_t s);
+hipError_t launch_unique_blocks(const void* L, int label_bits, const BlockGeom* blocks, const uint32_t* tile_prefix,
+                                int n_blocks, int64_t n_tiles, uint64_t* out, unsigned long long* count, int64_t cap,
+                                hipStream_t s);
+int unique_tile_y();
+hipError_t launch_block_bounds(int64_t n, const uint64_t* col, int stride, int n_blocks, int shift, int64_t* bounds,
+                               hipStream_t s);
+hipError_t launch_clear_bits(int64_t n, uint64_t* col, int stride, uint64_t mask, hipStream_t s);
 hipError_t launch_compact(int64_t E, const uint32_t* dE, const uint32_t* keep, const uint32_t* pos,
                           const ReduceOut& in, const ReduceOut& out, uint32_t* dkept, hipStream_t s);
 hipError_t launch_endpoints(int64_t E, const uint64_t* uniq, int nb, uint32_t* out, hipStream_t s);
@@ -252,6 +258,9 @@ struct ReduceJob {
     int64_t single_label_nodes;  // >=0: no edges -> nodes = this label; -1: none
     const uint64_t* single_label_ptr;  // device pointer to a label to use if E == 0
     const RegionPrefix* regions;       // keys in NREG regions of R (scan records), or null: dense
+    int ub = 0;                        // bits of the key's u field (0: = bits of the largest label)
+    uint64_t umask = ~0ull;            // label bits of u (batched blocks: below the block tag)
+    int skip_nodes = 0;                // batched blocks: nodes come from the per-block unique pass
 };
 
 static hipError_t reduce_records(Workspace& w, const ReduceJob& J, hipStream_t s, ctg_result* res) {
@@ -263,7 +272,8 @@ static hipError_t reduce_records(Workspace& w, const ReduceJob& J, hipStream_t s
     Ev ev{w, s};
     const int64_t n = J.n;
     const int nb = bits_for(J.max_v);
-    if (nb > 32) return hipErrorInvalidValue;
+    const int ub = J.ub ? J.ub : nb;
+    if (nb > 32 || ub > 32) return hipErrorInvalidValue;
     if (n == 0) {
         res->n_edges = 0;
         res->edges = (uint64_t*)dalloc(16);
@@ -304,7 +314,7 @@ static hipError_t reduce_records(Workspace& w, const ReduceJob& J, hipStream_t s
     // keys (slot in the low ib bits): 16 instead of 24 bytes per record and
     // pass; the reduction reads the slots from the sorted keys (CTG_SORT_PACKED=0 disables).
     const int ib = J.regions ? bits_for((uint64_t)std::max<int64_t>(J.R.cap - 1, 1)) : 0;
-    const bool packed = J.keys && J.regions && sort_packed() && 2 * nb + ib <= 64 && n <= sort_wide_digits_max();
+    const bool packed = J.keys && J.regions && sort_packed() && ub + nb + ib <= 64 && n <= sort_wide_digits_max();
     if (J.keys && J.regions)
         e = launch_pack_regions(J.keys, J.R.rcap, *J.regions, nb, packed ? ib : 0, w.sk_in, w.idx_in, s);
     else if (J.keys) e = launch_pack_keys(n, J.keys, nb, w.sk_in, w.idx_in, s);
@@ -313,16 +323,16 @@ static hipError_t reduce_records(Workspace& w, const ReduceJob& J, hipStream_t s
     ev.mark(2);
     if (packed) {
         ROCPRIM_CALL(w, rocprim::radix_sort_keys<RecordSortConfig>(t, tbytes, w.sk_in, w.sk_out, (size_t)n,
-                                                                   (unsigned)ib, (unsigned)(ib + 2 * nb), s));
+                                                                   (unsigned)ib, (unsigned)(ib + ub + nb), s));
         ev.mark(3);
         auto key_only = rocprim::make_transform_iterator(w.sk_out, [ib] __device__(uint64_t k) { return k >> ib; });
         ROCPRIM_CALL(w, rocprim::run_length_encode(t, tbytes, key_only, (unsigned)n, w.uniq, w.runs, dE_all, s));
     } else if (n <= sort_wide_digits_max()) {
         ROCPRIM_CALL(w, rocprim::radix_sort_pairs<RecordSortConfig>(t, tbytes, w.sk_in, w.sk_out, w.idx_in,
-                                                                    w.idx_out, (size_t)n, 0u, (unsigned)(2 * nb), s));
+                                                                    w.idx_out, (size_t)n, 0u, (unsigned)(ub + nb), s));
     } else {
         ROCPRIM_CALL(w, rocprim::radix_sort_pairs(t, tbytes, w.sk_in, w.sk_out, w.idx_in, w.idx_out, (size_t)n, 0u,
-                                                  (unsigned)(2 * nb), s));
+                                                  (unsigned)(ub + nb), s));
     }
     if (!packed) {
         ev.mark(3);
@@ -349,7 +359,8 @@ static hipError_t reduce_records(Workspace& w, const ReduceJob& J, hipStream_t s
         O.ablate = ablate;
     }
     e = launch_reduce(n, dE_all, w.uniq, w.runs, w.offs, packed ? nullptr : w.idx_out, packed ? w.sk_out : nullptr,
-                      packed ? ib : 0, J.R, J.wide, J.stats, nb, J.need_adj, J.ignore_label, J.scale, J.offset, O, s);
+                      packed ? ib : 0, J.R, J.wide, J.stats, nb, J.umask, J.need_adj, J.ignore_label, J.scale, J.offset,
+                      O, s);
     if (e != hipSuccess) return e;
     if (may_drop) {
         ROCPRIM_CALL(w, rocprim::exclusive_scan(t, tbytes, w.keep, w.pos, 0u, (size_t)n, rocprim::plus<uint32_t>(), s));
@@ -373,7 +384,15 @@ static hipError_t reduce_records(Workspace& w, const ReduceJob& J, hipStream_t s
 
     // nodes = unique endpoints of every unique key (before filtering)
     uint32_t counts[3] = {0, 0, 0};
-    if (J.max_v < (1ull << 30)) {
+    if (J.skip_nodes) {
+        res->nodes = (uint64_t*)dalloc(8);
+        e = hipMemcpyAsync(w.small_host, w.small, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, s);
+        if (e != hipSuccess) return e;
+        e = hipStreamSynchronize(s);
+        if (e != hipSuccess) return e;
+        counts[0] = w.small_host[0];
+        counts[1] = w.small_host[1];
+    } else if (J.max_v < (1ull << 30)) {
         // bitmap over [0, max label]: one pass over the sorted key table
         const int64_t W = (int64_t)(J.max_v >> 5) + 1;
         uint32_t* bits = (uint32_t*)dalloc(W * 4);
@@ -597,6 +616,57 @@ static int rag_dense_relabel(const void* dl, const void* dd, int data_kind, int 
     return CTG_OK;
 }
 
+// One face scan with its record bookkeeping: the record buffer grows and the
+// scan re-runs when a region overflowed.  *overflow = labels that do not fit
+// the key's u / v fields (the caller relabels densely).
+static int scan_records(Workspace& w, const ScanParams& P, int64_t V, hipStream_t s, Ev& ev, RegionPrefix& pre,
+                        bool* overflow, const char* who) {
+    *overflow = false;
+    if (getenv("CTG_REC_FRESH")) {   // test hook: start from the smallest record buffer
+        CTG_CHECK(hipStreamSynchronize(s));
+        dfree(w.rec.key); dfree(w.rec.sums); dfree(w.rec.hist);
+        w.rec = RecordBuf{};
+    }
+    int64_t need = std::max<int64_t>(w.rec.cap, std::max<int64_t>(1 << 16, V / 24));
+    need = (need + NREG - 1) / NREG * NREG;
+    for (int attempt = 0; attempt < 4; ++attempt) {
+        CTG_CHECK(ensure_records(w, need, 0));
+        CTG_CHECK(hipMemsetAsync(w.counters, 0, sizeof(Counters), s));
+        CTG_CHECK(launch_face_scan(P, w.rec, w.counters, s));
+        ev.mark(1);
+        CTG_CHECK(hipMemcpyAsync(w.counters_host, w.counters, sizeof(Counters), hipMemcpyDeviceToHost, s));
+        CTG_CHECK(hipStreamSynchronize(s));
+        if (w.counters_host->label_overflow) {
+            *overflow = true;
+            return CTG_OK;
+        }
+        unsigned long long tot = 0, mx = 0;
+        for (int r = 0; r < NREG; ++r) {
+            pre.off[r] = (uint32_t)tot;
+            tot += w.counters_host->rcount[r];
+            mx = std::max(mx, w.counters_host->rcount[r]);
+        }
+        pre.off[NREG] = (uint32_t)tot;
+        w.counters_host->n_records = tot;
+        if (tot >= (1ull << 32)) {
+            set_error(std::string(who) + ": more than 2^32 records");
+            return CTG_ERR_NOMEM;
+        }
+        if ((int64_t)mx <= w.rec.rcap) break;
+        need = ((int64_t)(mx * 5 / 4) + 1024) * NREG;
+        if (attempt == 3) {
+            set_error(std::string(who) + ": record buffer overflow");
+            return CTG_ERR_NOMEM;
+        }
+    }
+    if (P.ablate & 256)   // diagnostic s_memtime stamps, summed over waves
+        fprintf(stderr, "stamps total %llu fold %llu flush %llu wait %llu\n", w.counters_host->pad[2],
+                w.counters_host->pad[3], w.counters_host->pad[4], w.counters_host->pad[5]);
+    w.last_records = (int64_t)w.counters_host->n_records;
+    w.last_direct = (int64_t)w.counters_host->n_direct;
+    return CTG_OK;
+}
+
 int ctg_rag_features(const void* labels, int label_bits, const void* data, int data_kind, int n_channels,
                      const int32_t* offsets, const int64_t* shape, const int64_t* own_begin,
                      const int64_t* own_end, int ignore_label,
@@ -758,56 +828,20 @@ int ctg_rag_features(const void* labels, int label_bits, const void* data, int d
         *out = r;
         return CTG_OK;
     }
-    // record capacity: grows (and the scan re-runs) when exceeded
-    if (getenv("CTG_REC_FRESH")) {   // test hook: start from the smallest record buffer
-        CTG_CHECK(hipStreamSynchronize(s));
-        dfree(w.rec.key); dfree(w.rec.sums); dfree(w.rec.hist);
-        w.rec = RecordBuf{};
-    }
-    int64_t need = std::max<int64_t>(w.rec.cap, std::max<int64_t>(1 << 16, V / 24));
-    need = (need + NREG - 1) / NREG * NREG;
     RegionPrefix pre{};
     const bool stats = P.data_kind != CTG_DATA_NONE;
-    for (int attempt = 0; attempt < 4; ++attempt) {
-        CTG_CHECK(ensure_records(w, need, 0));
-        CTG_CHECK(hipMemsetAsync(w.counters, 0, sizeof(Counters), s));
-        CTG_CHECK(launch_face_scan(P, w.rec, w.counters, s));
-        ev.mark(1);
-        CTG_CHECK(hipMemcpyAsync(w.counters_host, w.counters, sizeof(Counters), hipMemcpyDeviceToHost, s));
-        CTG_CHECK(hipStreamSynchronize(s));
-        if (w.counters_host->label_overflow) {
-            if (label_bits != 64) {
-                set_error("ctg_rag_features: internal label overflow on 32-bit labels");
-                return CTG_ERR_HIP;
-            }
-            return rag_dense_relabel(dl, dd, data_kind, n_channels, offsets, shape, own_begin, own_end,
-                                     ignore_label, hist_lo, hist_hi, flags, stream, out);
+    bool overflow = false;
+    rc = scan_records(w, P, V, s, ev, pre, &overflow, "ctg_rag_features");
+    if (rc) return rc;
+    if (overflow) {
+        if (label_bits != 64) {
+            set_error("ctg_rag_features: internal label overflow on 32-bit labels");
+            return CTG_ERR_HIP;
         }
-        unsigned long long tot = 0, mx = 0;
-        for (int r = 0; r < NREG; ++r) {
-            pre.off[r] = (uint32_t)tot;
-            tot += w.counters_host->rcount[r];
-            mx = std::max(mx, w.counters_host->rcount[r]);
-        }
-        pre.off[NREG] = (uint32_t)tot;
-        w.counters_host->n_records = tot;
-        if (tot >= (1ull << 32)) {
-            set_error("ctg_rag_features: more than 2^32 records");
-            return CTG_ERR_NOMEM;
-        }
-        if ((int64_t)mx <= w.rec.rcap) break;
-        need = ((int64_t)(mx * 5 / 4) + 1024) * NREG;
-        if (attempt == 3) {
-            set_error("ctg_rag_features: record buffer overflow");
-            return CTG_ERR_NOMEM;
-        }
+        return rag_dense_relabel(dl, dd, data_kind, n_channels, offsets, shape, own_begin, own_end, ignore_label,
+                                 hist_lo, hist_hi, flags, stream, out);
     }
     const int64_t n = (int64_t)w.counters_host->n_records;
-    if (P.ablate & 256)   // diagnostic s_memtime stamps, summed over waves
-        fprintf(stderr, "stamps total %llu fold %llu flush %llu wait %llu\n", w.counters_host->pad[2],
-                w.counters_host->pad[3], w.counters_host->pad[4], w.counters_host->pad[5]);
-    w.last_records = n;
-    w.last_direct = (int64_t)w.counters_host->n_direct;
 
     ctg_result* r = new ctg_result();
     r->device = dev;
@@ -861,6 +895,317 @@ int ctg_rag_features(const void* labels, int label_bits, const void* data, int d
         w.last_ms[6] = ms;
     }
     *out = r;
+    return CTG_OK;
+}
+
+// ---------------------------------------------------------------------------
+// batched per-block sub-graphs / features (the ndist per-block calls)
+// ---------------------------------------------------------------------------
+static int bits_u(int64_t v) { return v <= 0 ? 0 : bits_for((uint64_t)v); }
+
+// the per-block nodes of a batched call: unique labels of every own box
+static int block_nodes(Workspace& w, const void* dl, int label_bits, const BlockGeom* dgeom, int n_blocks,
+                       const std::vector<uint32_t>& uprefix, int64_t own_voxels, hipStream_t s, ctg_result* r) {
+    const int64_t n_tiles = uprefix.back();
+    uint32_t* dprefix = (uint32_t*)dalloc((n_blocks + 1) * 4);
+    if (!dprefix) return CTG_ERR_NOMEM;
+    CTG_CHECK(hipMemcpyAsync(dprefix, uprefix.data(), (n_blocks + 1) * 4, hipMemcpyHostToDevice, s));
+    int64_t cap = std::max<int64_t>(1, std::min<int64_t>(own_voxels, std::max<int64_t>(1 << 16, own_voxels / 8)));
+    for (int attempt = 0; attempt < 3; ++attempt) {
+        uint64_t* cand = (uint64_t*)dalloc(cap * 8);
+        uint64_t* sorted = (uint64_t*)dalloc(cap * 8);
+        uint64_t* nodes = (uint64_t*)dalloc(cap * 8);
+        int64_t* bounds = (int64_t*)dalloc((n_blocks + 1) * 8);
+        if (!cand || !sorted || !nodes || !bounds) return CTG_ERR_NOMEM;
+        CTG_CHECK(hipMemsetAsync(w.counters, 0, sizeof(Counters), s));
+        CTG_CHECK(launch_unique_blocks(dl, label_bits, dgeom, dprefix, n_blocks, n_tiles, cand,
+                                       &w.counters->n_records, cap, s));
+        CTG_CHECK(hipMemcpyAsync(w.counters_host, w.counters, sizeof(Counters), hipMemcpyDeviceToHost, s));
+        CTG_CHECK(hipStreamSynchronize(s));
+        const int64_t m = (int64_t)w.counters_host->n_records;
+        if (m > cap) {
+            dfree(cand); dfree(sorted); dfree(nodes); dfree(bounds);
+            cap = m + 1024;
+            continue;
+        }
+        const unsigned kb = 32u + (unsigned)bits_u(n_blocks - 1);
+        size_t tb = 0;
+        CTG_CHECK(rocprim::radix_sort_keys(nullptr, tb, cand, sorted, (size_t)m, 0u, kb, s));
+        ensure(&w.temp, w.temp_bytes, tb + 256);
+        tb = w.temp_bytes;
+        CTG_CHECK(rocprim::radix_sort_keys(w.temp, tb, cand, sorted, (size_t)m, 0u, kb, s));
+        tb = 0;
+        CTG_CHECK(rocprim::unique(nullptr, tb, sorted, nodes, w.small + 2, (size_t)m, rocprim::equal_to<uint64_t>(), s));
+        ensure(&w.temp, w.temp_bytes, tb + 256);
+        tb = w.temp_bytes;
+        CTG_CHECK(rocprim::unique(w.temp, tb, sorted, nodes, w.small + 2, (size_t)m, rocprim::equal_to<uint64_t>(), s));
+        CTG_CHECK(hipMemcpyAsync(w.small_host + 2, w.small + 2, 4, hipMemcpyDeviceToHost, s));
+        CTG_CHECK(hipStreamSynchronize(s));
+        const int64_t N = w.small_host[2];
+        CTG_CHECK(launch_block_bounds(N, nodes, 1, n_blocks, 32, bounds, s));
+        r->node_off.assign(n_blocks + 1, 0);
+        CTG_CHECK(hipMemcpyAsync(r->node_off.data(), bounds, (n_blocks + 1) * 8, hipMemcpyDeviceToHost, s));
+        CTG_CHECK(launch_clear_bits(N, nodes, 1, 0xFFFFFFFFull, s));
+        CTG_CHECK(hipStreamSynchronize(s));
+        dfree(r->nodes);
+        r->nodes = nodes;
+        r->n_nodes = N;
+        dfree(cand); dfree(sorted); dfree(bounds); dfree(dprefix);
+        return CTG_OK;
+    }
+    set_error("ctg_rag_blocks: node candidate buffer overflow");
+    return CTG_ERR_NOMEM;
+}
+
+int ctg_rag_blocks(const void* labels, int label_bits, const void* data, int data_kind, int n_channels,
+                   const int32_t* offsets, const ctg_block_desc* blocks, int n_blocks, int64_t labels_len,
+                   int64_t data_len, int ignore_label, double hist_lo, double hist_hi, int flags, int mem,
+                   void* stream, ctg_result** out) {
+    if (!out || !labels || !blocks || n_blocks < 1 || n_blocks > (1 << 20) || labels_len < 0 ||
+        (label_bits != 32 && label_bits != 64) || (data && data_kind != CTG_DATA_F32 && data_kind != CTG_DATA_U8) ||
+        n_channels < 0 || n_channels > CTG_MAX_CHANNELS || (n_channels > 0 && !offsets) || !(hist_hi > hist_lo)) {
+        set_error("ctg_rag_blocks: bad arguments");
+        return CTG_ERR_ARG;
+    }
+    *out = nullptr;
+    const int nch = data ? std::max(1, n_channels) : 0;
+    int64_t own_voxels = 0, voxels = 0, zmax = 1;
+    for (int b = 0; b < n_blocks; ++b) {
+        const ctg_block_desc& d = blocks[b];
+        int64_t V = 1;
+        for (int k = 0; k < 3; ++k) {
+            V *= d.shape[k];
+            if (d.shape[k] < 0 || d.shape[k] > 0x7FFFFFFF || d.own_begin[k] < 0 || d.own_end[k] > d.shape[k] ||
+                d.graph_begin[k] < 0 || d.graph_end[k] > d.shape[k]) {
+                set_error("ctg_rag_blocks: block " + std::to_string(b) + ": box outside its array");
+                return CTG_ERR_ARG;
+            }
+        }
+        if (d.label_offset < 0 || d.label_offset + V > labels_len ||
+            (data && (d.data_offset < 0 || d.data_offset + V * nch > data_len))) {
+            set_error("ctg_rag_blocks: block " + std::to_string(b) + ": array outside the arena");
+            return CTG_ERR_ARG;
+        }
+        int64_t ov = 1;
+        for (int k = 0; k < 3; ++k) ov *= std::max<int64_t>(0, d.own_end[k] - d.own_begin[k]);
+        own_voxels += ov;
+        voxels += V;
+        zmax = std::max(zmax, d.shape[0]);
+    }
+    const int dev = cur_dev();
+    Workspace& w = ws(dev);
+    CTG_CHECK(ws_init(w));
+    hipStream_t s = (hipStream_t)stream;
+    const void* dl = nullptr;
+    const void* dd = nullptr;
+    int rc = stage_in(w, 0, labels, (size_t)labels_len * (label_bits / 8), mem, s, &dl);
+    if (rc) return rc;
+    rc = stage_in(w, 1, data, data ? (size_t)data_len * (data_kind == CTG_DATA_U8 ? 1 : 4) : 0, mem, s, &dd);
+    if (rc) return rc;
+
+    ScanParams P;
+    std::memset(&P, 0, sizeof(P));
+    P.labels = dl;
+    P.data = dd;
+    P.label_bits = label_bits;
+    P.data_kind = data ? data_kind : CTG_DATA_NONE;
+    P.n_channels = data ? n_channels : 0;
+    for (int c = 0; c < P.n_channels; ++c)
+        for (int k = 0; k < 3; ++k) P.offsets[c][k] = offsets[3 * c + k];
+    for (int c = 0; c < P.n_channels; ++c) {
+        const int* o = P.offsets[c];
+        if (std::abs(o[0]) + std::abs(o[1]) + std::abs(o[2]) > 1) P.lr_mask |= 1u << c;
+    }
+    P.scale = (double)NBINS / (hist_hi - hist_lo);
+    P.offset = hist_lo;
+    P.fast40 = (hist_lo == 0.0 && P.scale == 40.0) ? 1 : 0;
+    P.check_planes = 8;
+    P.tile_z = (int)std::min<int64_t>(zmax, 128);   // one tile deep for the usual <= 128-plane blocks
+    if (const char* t = getenv("CTG_TILE_Z")) P.tile_z = std::max(1, atoi(t));
+    P.xcd_remap = 1;
+    const int tag_bits = bits_u(n_blocks - 1);
+    P.tag_shift = 32 - tag_bits;
+    P.label_hi_mask = tag_bits ? ~((1u << P.tag_shift) - 1u) : 0u;
+    P.n_blocks = n_blocks;
+    // per-block geometry and the tile prefixes of the scan / node launches
+    const int rows = scan_tile_rows(), uty = unique_tile_y();
+    std::vector<BlockGeom> geom(n_blocks);
+    std::vector<uint32_t> prefix(n_blocks + 1, 0), uprefix(n_blocks + 1, 0);
+    for (int b = 0; b < n_blocks; ++b) {
+        const ctg_block_desc& d = blocks[b];
+        BlockGeom& g = geom[b];
+        g.label_offset = d.label_offset;
+        g.data_offset = data ? d.data_offset : 0;
+        for (int k = 0; k < 3; ++k) {
+            g.shape[k] = (int32_t)d.shape[k];
+            g.own_begin[k] = (int32_t)d.own_begin[k];
+            g.own_end[k] = (int32_t)d.own_end[k];
+            g.graph_begin[k] = (int32_t)d.graph_begin[k];
+            g.graph_end[k] = (int32_t)d.graph_end[k];
+        }
+        g.ntx = (int32_t)((d.shape[2] + TILE_X - 1) / TILE_X);
+        g.nty = (int32_t)((d.shape[1] + rows - 1) / rows);
+        g.ntz = (int32_t)((d.shape[0] + P.tile_z - 1) / P.tile_z);
+        const int64_t nt = (int64_t)g.ntx * g.nty * g.ntz;
+        int64_t ut = 1;
+        const int64_t oe[3] = {std::max<int64_t>(0, d.own_end[0] - d.own_begin[0]),
+                               std::max<int64_t>(0, d.own_end[1] - d.own_begin[1]),
+                               std::max<int64_t>(0, d.own_end[2] - d.own_begin[2])};
+        ut = ((oe[2] + 63) / 64) * ((oe[1] + uty - 1) / uty) * ((oe[0] + 15) / 16);
+        if ((int64_t)prefix[b] + nt > 0x7FFFFFFFll || (int64_t)uprefix[b] + ut > 0x7FFFFFFFll) {
+            set_error("ctg_rag_blocks: too many tiles in one call");
+            return CTG_ERR_ARG;
+        }
+        prefix[b + 1] = prefix[b] + (uint32_t)nt;
+        uprefix[b + 1] = uprefix[b] + (uint32_t)ut;
+    }
+    P.batch_tiles = prefix[n_blocks];
+    BlockGeom* dgeom = (BlockGeom*)dalloc(sizeof(BlockGeom) * n_blocks);
+    uint32_t* dprefix = (uint32_t*)dalloc((n_blocks + 1) * 4);
+    if (!dgeom || !dprefix) {
+        set_error("ctg_rag_blocks: out of device memory");
+        return CTG_ERR_NOMEM;
+    }
+    CTG_CHECK(hipMemcpyAsync(dgeom, geom.data(), sizeof(BlockGeom) * n_blocks, hipMemcpyHostToDevice, s));
+    CTG_CHECK(hipMemcpyAsync(dprefix, prefix.data(), (n_blocks + 1) * 4, hipMemcpyHostToDevice, s));
+    P.blocks = dgeom;
+    P.tile_prefix = dprefix;
+    struct Release {
+        BlockGeom* g;
+        uint32_t* p;
+        hipStream_t s;
+        ~Release() {
+            hipStreamSynchronize(s);
+            dfree(g);
+            dfree(p);
+        }
+    } release{dgeom, dprefix, s};
+
+    Ev ev{w, s};
+    ev.mark(0);
+    RegionPrefix pre{};
+    bool overflow = false;
+    rc = P.batch_tiles ? scan_records(w, P, voxels, s, ev, pre, &overflow, "ctg_rag_blocks") : CTG_OK;
+    if (rc) return rc;
+    if (overflow) {
+        // labels too large for the tagged keys: relabel the arena densely
+        // (monotone, so sorted dense tables stay sorted after mapping back)
+        const uint64_t* l64 = (const uint64_t*)dl;
+        uint64_t* wide = nullptr;
+        if (label_bits == 32) {
+            wide = (uint64_t*)dalloc(std::max<int64_t>(labels_len, 1) * 8);
+            if (!wide) return CTG_ERR_NOMEM;
+            CTG_CHECK(launch_u32_to_u64(labels_len, (const uint32_t*)dl, wide, s));
+            l64 = wide;
+        }
+        ctg_result* U = nullptr;
+        rc = ctg_unique_values(l64, labels_len, CTG_MEM_DEVICE, stream, &U);
+        if (rc) return rc;
+        if (U->n_nodes > (int64_t)(1ull << P.tag_shift)) {
+            ctg_free(U);
+            set_error("ctg_rag_blocks: too many distinct labels for one batch of blocks: call with fewer blocks");
+            return CTG_ERR_UNSUPPORTED;
+        }
+        uint32_t* dense = (uint32_t*)dalloc(std::max<int64_t>(labels_len, 1) * 4);
+        if (!dense) {
+            ctg_free(U);
+            return CTG_ERR_NOMEM;
+        }
+        CTG_CHECK(launch_remap_dense(l64, labels_len, U->nodes, U->n_nodes, dense, s));
+        ctg_result* r = nullptr;
+        rc = ctg_rag_blocks(dense, 32, dd, data_kind, n_channels, offsets, blocks, n_blocks, labels_len, data_len,
+                            ignore_label, hist_lo, hist_hi, flags, CTG_MEM_DEVICE, stream, &r);
+        dfree(dense);
+        if (wide) dfree(wide);
+        if (rc) {
+            ctg_free(U);
+            return rc;
+        }
+        CTG_CHECK(launch_gather_labels(U->nodes, r->edges, 2 * r->n_edges, s));
+        CTG_CHECK(launch_gather_labels(U->nodes, r->nodes, r->n_nodes, s));
+        CTG_CHECK(hipStreamSynchronize(s));
+        ctg_free(U);
+        *out = r;
+        return CTG_OK;
+    }
+    const int64_t n = P.batch_tiles ? (int64_t)w.counters_host->n_records : 0;
+    ctg_result* r = new ctg_result();
+    r->device = dev;
+    r->n_records = n;
+    r->n_direct = P.batch_tiles ? (int64_t)w.counters_host->n_direct : 0;
+    ReduceJob J{};
+    J.n = n;
+    J.keys = w.rec.key;
+    J.regions = &pre;
+    J.R = w.rec;
+    J.stats = P.data_kind != CTG_DATA_NONE;
+    // boundary / graph: every key is a face of the block's graph box;
+    // affinities: keep the keys of the block's sub-graph (ADJ marks)
+    J.need_adj = P.n_channels > 0 ? 1 : 0;
+    J.ignore_label = ignore_label;
+    J.keep_stats = (flags & CTG_KEEP_STATS) ? 1 : 0;
+    J.max_v = P.batch_tiles ? w.counters_host->max_v : 0;
+    J.scale = P.scale;
+    J.offset = P.offset;
+    J.ub = tag_bits ? 32 : 0;
+    J.umask = tag_bits ? (1ull << P.tag_shift) - 1ull : ~0ull;
+    J.skip_nodes = 1;
+    hipError_t e = reduce_records(w, J, s, r);
+    if (e == hipSuccess) {
+        r->edge_off.assign(n_blocks + 1, 0);
+        r->edge_off[n_blocks] = r->n_edges;
+        if (tag_bits && r->n_edges) {
+            int64_t* bounds = (int64_t*)dalloc((n_blocks + 1) * 8);
+            e = bounds ? launch_block_bounds(r->n_edges, r->edges, 2, n_blocks, P.tag_shift, bounds, s)
+                       : hipErrorOutOfMemory;
+            if (e == hipSuccess)
+                e = hipMemcpyAsync(r->edge_off.data(), bounds, (n_blocks + 1) * 8, hipMemcpyDeviceToHost, s);
+            if (e == hipSuccess) e = launch_clear_bits(r->n_edges, r->edges, 2, J.umask, s);
+            if (e == hipSuccess) e = hipStreamSynchronize(s);
+            dfree(bounds);
+        }
+    }
+    if (e != hipSuccess) {
+        set_error(std::string("ctg_rag_blocks: ") + hipGetErrorString(e));
+        ctg_free(r);
+        return CTG_ERR_HIP;
+    }
+    rc = block_nodes(w, dl, label_bits, dgeom, n_blocks, uprefix, own_voxels, s, r);
+    if (rc) {
+        ctg_free(r);
+        return rc;
+    }
+    *out = r;
+    return CTG_OK;
+}
+
+void* ctg_host_alloc(int64_t bytes) {
+    void* p = nullptr;
+    if (bytes <= 0) bytes = 64;
+    if (hipHostMalloc(&p, (size_t)bytes, hipHostMallocDefault) != hipSuccess) {
+        set_error("ctg_host_alloc: hipHostMalloc failed");
+        return nullptr;
+    }
+    return p;
+}
+
+void ctg_host_free(void* p) {
+    if (p) hipHostFree(p);
+}
+
+int ctg_result_num_blocks(const ctg_result* r) { return r ? (int)std::max<size_t>(r->edge_off.size(), 1) - 1 : -1; }
+
+int ctg_result_block_offsets(const ctg_result* r, int64_t* edge_off, int64_t* node_off) {
+    if (!r || r->edge_off.empty()) {
+        set_error("ctg_result_block_offsets: not a batched-blocks result");
+        return CTG_ERR_ARG;
+    }
+    const size_t nb = r->edge_off.size();
+    if (edge_off) std::memcpy(edge_off, r->edge_off.data(), nb * 8);
+    if (node_off) {
+        if (r->node_off.size() == nb) std::memcpy(node_off, r->node_off.data(), nb * 8);
+        else std::memset(node_off, 0, nb * 8);
+    }
     return CTG_OK;
 }
 

@@ -85,6 +85,17 @@ struct RecordBuf {
     int64_t rcap = 0;             // slots per region (cap / NREG)
 };
 
+// one array of a batched call (ctg_rag_blocks): the host's ctg_block_desc
+// in device memory plus the tile bookkeeping of the launch
+struct BlockGeom {
+    int64_t label_offset;    // element offset of the array in the labels arena
+    int64_t data_offset;     // element offset in the data arena (affinities: channel 0 of C x V)
+    int32_t shape[3];
+    int32_t own_begin[3], own_end[3];
+    int32_t graph_begin[3], graph_end[3];
+    int32_t ntx, nty, ntz;   // tiles along x, y, z
+};
+
 struct ScanParams {
     const void* labels;
     const void* data;          // boundary (Z,Y,X) or affinities (C,Z,Y,X); may be null
@@ -112,6 +123,16 @@ struct ScanParams {
     // key is a RAG edge and the scan pushes no adjacency markers
     int skip_adj_marks;
     uint32_t lr_mask;          // bit c: channel c is long-range (|offset|_1 > 1)
+    // batched blocks (ctg_rag_blocks): workgroup w scans a tile of array b with
+    // tile_prefix[b] <= w < tile_prefix[b+1]; keys carry b in the bits of u
+    // from tag_shift up, so labels must stay below 2^tag_shift (else the label
+    // overflow flag is raised and the host relabels densely)
+    const BlockGeom* blocks;
+    const uint32_t* tile_prefix;
+    int n_blocks;
+    int64_t batch_tiles;       // tile_prefix[n_blocks]: the launch's workgroups
+    int tag_shift;             // 32: no tag (n_blocks == 1)
+    uint32_t label_hi_mask;    // bits a narrowed label must not have (overflow flag)
 };
 
 struct Counters {               // device-side counters, zeroed per call
@@ -170,6 +191,10 @@ hipError_t ensure_records(Workspace& w, int64_t need, int wide);
 // result handle (opaque in the C ABI)
 struct ctg_result {
     int device = -1;
+    // batched blocks (ctg_rag_blocks): rows [edge_off[b], edge_off[b+1]) of the
+    // edge / feature tables and [node_off[b], node_off[b+1]) of the node table
+    // belong to block b
+    std::vector<int64_t> edge_off, node_off;
     int64_t n_edges = 0;
     int64_t n_nodes = 0;
     uint64_t* edges = nullptr;      // device (E,2)

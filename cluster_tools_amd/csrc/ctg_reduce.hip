@@ -264,7 +264,7 @@ __global__ __launch_bounds__(256) void k_reduce_edges(int64_t E, const uint32_t*
                                                       const uint64_t* __restrict__ uniq,
                                                       const uint32_t* __restrict__ runs,
                                                       const uint32_t* __restrict__ offs,
-                                                      Perm perm, RecordBuf R, int nb,
+                                                      Perm perm, RecordBuf R, int nb, uint64_t umask,
                                                       int need_adj, int ignore_label, double scale, double offset,
                                                       ReduceOut O) {
     const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -285,7 +285,7 @@ __global__ __launch_bounds__(256) void k_reduce_edges(int64_t E, const uint32_t*
         } else {
             flags = ADJ_FLAG;
         }
-        if (O.keep) O.keep[e] = ((flags & ADJ_FLAG) || need_adj != 1) && !(ignore_label && u == 0) ? 1u : 0u;
+        if (O.keep) O.keep[e] = ((flags & ADJ_FLAG) || need_adj != 1) && !(ignore_label && (u & umask) == 0) ? 1u : 0u;
         return;
     } else {
         uint32_t h[NSLOTS];
@@ -308,7 +308,7 @@ __global__ __launch_bounds__(256) void k_reduce_edges(int64_t E, const uint32_t*
         // need_adj: 0 every record is an edge (boundary maps), 1 keep edges seen
         // on a nearest-neighbour face, 2 keep all and carry the flag (partials)
         if (need_adj == 0) flags |= ADJ_FLAG;
-        const bool keep = (need_adj == 2 || (flags & ADJ_FLAG)) && !(ignore_label && u == 0);
+        const bool keep = (need_adj == 2 || (flags & ADJ_FLAG)) && !(ignore_label && (u & umask) == 0);
         if (O.keep) O.keep[e] = keep ? 1u : 0u;
         if (O.wstats) {
             uint4* p = (uint4*)(O.wstats + (size_t)e * WREC_WORDS);
@@ -647,6 +647,40 @@ hipError_t launch_merge_feature_rows(int64_t n, const uint32_t* key, const uint3
     return hipGetLastError();
 }
 
+// batched blocks: row range of every block in a table sorted by its tagged
+// first column (tag = block << shift), then the tag bits are cleared
+__global__ void k_block_bounds(int64_t n, const uint64_t* __restrict__ col, int stride, int n_blocks, int shift,
+                               int64_t* __restrict__ bounds) {
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b > n_blocks) return;
+    const uint64_t key = (uint64_t)b << shift;
+    int64_t lo = 0, hi = n;
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if (col[mid * stride] < key) lo = mid + 1;
+        else hi = mid;
+    }
+    bounds[b] = b == n_blocks ? n : lo;
+}
+
+__global__ void k_clear_bits(int64_t n, uint64_t* __restrict__ col, int stride, uint64_t mask) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) col[i * stride] &= mask;
+}
+
+hipError_t launch_block_bounds(int64_t n, const uint64_t* col, int stride, int n_blocks, int shift, int64_t* bounds,
+                               hipStream_t s) {
+    hipLaunchKernelGGL(k_block_bounds, dim3((unsigned)((n_blocks + 1 + 255) / 256)), dim3(256), 0, s, n, col, stride,
+                       n_blocks, shift, bounds);
+    return hipGetLastError();
+}
+
+hipError_t launch_clear_bits(int64_t n, uint64_t* col, int stride, uint64_t mask, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_clear_bits, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, n, col, stride, mask);
+    return hipGetLastError();
+}
+
 hipError_t launch_pack_keys(int64_t n, const uint64_t* key, int nb, uint64_t* sk, uint32_t* idx, hipStream_t s) {
     if (n == 0) return hipSuccess;
     hipLaunchKernelGGL(k_pack_keys, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, n, key, nb, sk, idx);
@@ -674,17 +708,17 @@ hipError_t launch_max_pairs(int64_t n, const uint64_t* uv, unsigned long long* o
 }
 hipError_t launch_reduce(int64_t E, const uint32_t* dE, const uint64_t* uniq, const uint32_t* runs,
                          const uint32_t* offs, const uint32_t* perm32, const uint64_t* perm64, int ib,
-                         const RecordBuf& R, int wide, int stats, int nb, int need_adj, int ignore_label, double scale,
-                         double offset, const ReduceOut& O, hipStream_t s) {
+                         const RecordBuf& R, int wide, int stats, int nb, uint64_t umask, int need_adj,
+                         int ignore_label, double scale, double offset, const ReduceOut& O, hipStream_t s) {
     if (E == 0) return hipSuccess;
     const Perm perm{perm32, perm64, ib};
     dim3 g((unsigned)((E + 255) / 256)), b(256);
     if (wide) {
-        if (stats) hipLaunchKernelGGL((k_reduce_edges<true, true>), g, b, 0, s, E, dE, uniq, runs, offs, perm, R, nb, need_adj, ignore_label, scale, offset, O);
-        else hipLaunchKernelGGL((k_reduce_edges<true, false>), g, b, 0, s, E, dE, uniq, runs, offs, perm, R, nb, need_adj, ignore_label, scale, offset, O);
+        if (stats) hipLaunchKernelGGL((k_reduce_edges<true, true>), g, b, 0, s, E, dE, uniq, runs, offs, perm, R, nb, umask, need_adj, ignore_label, scale, offset, O);
+        else hipLaunchKernelGGL((k_reduce_edges<true, false>), g, b, 0, s, E, dE, uniq, runs, offs, perm, R, nb, umask, need_adj, ignore_label, scale, offset, O);
     } else {
-        if (stats) hipLaunchKernelGGL((k_reduce_edges<false, true>), g, b, 0, s, E, dE, uniq, runs, offs, perm, R, nb, need_adj, ignore_label, scale, offset, O);
-        else hipLaunchKernelGGL((k_reduce_edges<false, false>), g, b, 0, s, E, dE, uniq, runs, offs, perm, R, nb, need_adj, ignore_label, scale, offset, O);
+        if (stats) hipLaunchKernelGGL((k_reduce_edges<false, true>), g, b, 0, s, E, dE, uniq, runs, offs, perm, R, nb, umask, need_adj, ignore_label, scale, offset, O);
+        else hipLaunchKernelGGL((k_reduce_edges<false, false>), g, b, 0, s, E, dE, uniq, runs, offs, perm, R, nb, umask, need_adj, ignore_label, scale, offset, O);
     }
     return hipGetLastError();
 }

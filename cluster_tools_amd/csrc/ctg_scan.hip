@@ -361,12 +361,15 @@ __device__ __forceinline__ void fold_stats(Table& T, const StageT& e, int s, Rec
         if (s < 0) emit_direct(R, C, key, 0u, -1, -1, 0.0, 0.0, 0u, 0u, false);
         return;
     } else {
-        const bool adj = AFF && e.w == MARK_ADJ;
+        // adjacency-only entries: a nearest-neighbour face of an affinity map, or
+        // (batched blocks) a boundary face of the block's sub-graph that the
+        // block does not own -- the key is inserted, no sample counted
+        const bool adj = e.w == MARK_ADJ && (AFF || e.z == MARK_ADJ);
         const float a = __uint_as_float(e.z);
         const float b = BND ? __uint_as_float(e.w) : a;
-        const uint32_t n = BND ? 2u : (adj ? 0u : 1u);
+        const uint32_t n = adj ? 0u : (BND ? 2u : 1u);
         const int sa = adj ? -1 : sample_slot<FAST40>(a, scale, offset);
-        const int sb = BND ? sample_slot<FAST40>(b, scale, offset) : -1;
+        const int sb = (BND && !adj) ? sample_slot<FAST40>(b, scale, offset) : -1;
         const double da = (double)a, db = (double)b;
         const double ds = BND ? da + db : da;
         const double dq = BND ? da * da + db * db : da * da;
@@ -397,104 +400,9 @@ __device__ __forceinline__ void fold_stats(Table& T, const StageT& e, int s, Rec
     }
 }
 
-#ifndef CTG_RUNCOMB
-#define CTG_RUNCOMB 0
-#endif
-// fold_stats with run combining (see CTG_RUNCOMB below): every lane of the
-// wave calls it (DPP needs the whole wave); `valid` marks real entries.
-template <int D>
-__device__ __forceinline__ uint32_t dpp_shr_u(uint32_t v) {
-    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x110 + D, 0xf, 0xf, false);
-}
-template <int D>
-__device__ __forceinline__ double dpp_shr_d(double v) {
-    const uint64_t b = (uint64_t)__double_as_longlong(v);
-    const uint32_t lo = dpp_shr_u<D>((uint32_t)b), hi = dpp_shr_u<D>((uint32_t)(b >> 32));
-    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
-}
-
-template <int MODE, bool FAST40, typename StageT>
-__device__ __forceinline__ void fold_stats_runs(Table& T, const StageT& e, int s, bool valid, int lane, RecordBuf R,
-                                                Counters* C, double scale, double offset, int ablate) {
-    constexpr bool BND = MODE == MODE_BOUNDARY;
-    constexpr bool AFF = MODE == MODE_AFFINITY;
-    constexpr int G = CTG_RUNCOMB;
-    const bool adj = AFF && e.w == MARK_ADJ;
-    const float a = __uint_as_float(e.z);
-    const float b = BND ? __uint_as_float(e.w) : a;
-    const int sa = adj ? -1 : sample_slot<FAST40>(a, scale, offset);
-    const int sb = BND ? sample_slot<FAST40>(b, scale, offset) : -1;
-    const double da = (double)a, db = (double)b;
-    uint32_t n = (!valid || adj) ? 0u : (BND ? 2u : 1u);
-    double ds = n ? (BND ? da + db : da) : 0.0;
-    double dq = n ? (BND ? da * da + db * db : da * da) : 0.0;
-    uint32_t mn = n ? f2ord(fminf(a, b)) : ORD_POS_INF, mx = n ? f2ord(fmaxf(a, b)) : ORD_NEG_INF;
-    uint32_t fl = (valid && adj) ? ADJ_FLAG : 0u;
-    // run heads: group start, key change, invalid entry or a direct record
-    // (on either side) -- directs are emitted one face each
-    const int sk = valid ? s : -2;
-    const uint32_t px = dpp_shr_u<1>(e.x), py = dpp_shr_u<1>(e.y), ps = dpp_shr_u<1>((uint32_t)sk);
-    const bool head = (lane & (G - 1)) == 0 || px != e.x || py != e.y || (int)ps != sk || sk < 0;
-    const uint64_t hm = __ballot(head);
-    const uint64_t le = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);
-    const int hp = 63 - __clzll(hm & le);   // this lane's run head
-#pragma unroll
-    for (int d = 1; d < G; d <<= 1) {
-        uint32_t on, omn, omx, ofl;
-        double ods, odq;
-        if (d == 1) {
-            on = dpp_shr_u<1>(n); omn = dpp_shr_u<1>(mn); omx = dpp_shr_u<1>(mx); ofl = dpp_shr_u<1>(fl);
-            ods = dpp_shr_d<1>(ds); odq = dpp_shr_d<1>(dq);
-        } else if (d == 2) {
-            on = dpp_shr_u<2>(n); omn = dpp_shr_u<2>(mn); omx = dpp_shr_u<2>(mx); ofl = dpp_shr_u<2>(fl);
-            ods = dpp_shr_d<2>(ds); odq = dpp_shr_d<2>(dq);
-        } else {
-            on = dpp_shr_u<4>(n); omn = dpp_shr_u<4>(mn); omx = dpp_shr_u<4>(mx); ofl = dpp_shr_u<4>(fl);
-            ods = dpp_shr_d<4>(ds); odq = dpp_shr_d<4>(dq);
-        }
-        if (lane - d >= hp) {
-            n += on;
-            ds += ods;
-            dq += odq;
-            mn = min(mn, omn);
-            mx = max(mx, omx);
-            fl |= ofl;
-        }
-    }
-    if (!valid) return;
-    const bool tail = lane == 63 || ((lane + 1) & (G - 1)) == 0 || ((hm >> (lane + 1)) & 1ull);
-    const uint64_t key = ((uint64_t)e.x << 32) | e.y;
-    if (s < 0) {   // direct record: its own run of one face
-        emit_direct(R, C, key, n | fl, sa, sb, ds, dq, mn, mx, true);
-        return;
-    }
-    if (tail) {
-        if (fl) atomicOr(&T.w[s][21], ADJ_FLAG);
-        if (n) {
-            atomicAdd(&T.sum[s], ds);
-            atomicAdd(&T.sq[s], dq);
-            atomicMin(&T.w[s][22], mn);
-            atomicMax(&T.w[s][23], mx);
-            atomicAdd(&T.w[s][21], n);
-        }
-    }
-    if (adj || (ablate & 128)) return;
-    if constexpr (BND) hist_add2(T, s, sa, sb);
-    else atomicAdd(&T.w[s][sa >> 1], 1u << ((sa & 1) * 16));
-}
-
 // Fold the wave's nb staged entries into the LDS edge table: NPER entries per
 // lane (lane, lane+64, ...), their stage reads and home-bucket reads issued
 // together so the LDS round trips of the entries overlap.
-// Run combining (CTG_RUNCOMB = G > 0): consecutive stage entries are mostly
-// the same face key (a boundary patch along x, a long-range pair along x), and
-// their statistics atomics then all hit one LDS address and serialise.  Within
-// aligned groups of G lanes the contributions (count, sum, sum of squares,
-// min, max, ADJ) of equal-key neighbours are combined with a segmented DPP
-// scan, and only the last lane of each run issues the statistics atomics; the
-// histogram keeps one atomic per sample.
-constexpr int RUNCOMB = CTG_RUNCOMB;
-
 template <int MODE, bool FAST40, typename StageT, int NPER>
 __device__ __forceinline__ void fold_batch(Table& T, const StageT* __restrict__ stage, int nb, int lane, RecordBuf R,
                                            Counters* C, double scale, double offset, bool& need, int ablate) {
@@ -542,11 +450,7 @@ __device__ __forceinline__ void fold_batch(Table& T, const StageT* __restrict__ 
                 }
             }
         }
-        if constexpr (RUNCOMB > 0 && MODE != MODE_GRAPH) {
-            fold_stats_runs<MODE, FAST40, StageT>(T, e[i], s, valid, lane, R, C, scale, offset, ablate);
-        } else {
-            if (valid) fold_stats<MODE, FAST40, StageT>(T, e[i], s, R, C, scale, offset, need, ablate);
-        }
+        if (valid) fold_stats<MODE, FAST40, StageT>(T, e[i], s, R, C, scale, offset, need, ablate);
     }
 }
 
@@ -603,53 +507,95 @@ __global__ __launch_bounds__(SCAN_THREADS, 4) void k_face_scan(ScanParams P, Rec
     }
     __syncthreads();
 
-    const int Z = (int)P.shape[0], Y = (int)P.shape[1], X = (int)P.shape[2];
-    const int64_t sz = (int64_t)Y * X;
     // XCD-aware tile order: the hardware deals workgroups round-robin over the
     // 8 XCDs (block b and b+8 share one), so block b takes tile t(b) with each
     // XCD owning one contiguous run of tiles (x fastest, then y, then z).  The
     // workgroups an XCD runs at a time are then x / y neighbours, and the
     // x-halo column and y-halo row one tile reads are the rows its neighbour
     // streams through the same L2, not a second HBM read.
-    int tx, ty, tz;
+    uint32_t t;
     {
         const uint32_t nwg = gridDim.x, id = blockIdx.x;
-        uint32_t t = id;
+        t = id;
         if (P.xcd_remap) {
             const uint32_t q = nwg / 8, rm = nwg % 8, xcd = id % 8, j = id / 8;
             t = xcd < rm ? xcd * (q + 1) + j : rm * (q + 1) + (xcd - rm) * q + j;
         }
-        const uint32_t ntx = (uint32_t)P.ntiles[0], nty = (uint32_t)P.ntiles[1];
-        tx = (int)(t % ntx);
-        ty = (int)((t / ntx) % nty);
-        tz = (int)(t / (ntx * nty));
     }
+    // geometry: the whole array, or (ctg_rag_blocks) the array of the block
+    // whose tile range holds t.  Faces with both voxels in the graph box are
+    // pushed (sub-graph edges); those owned by the block -- upper voxel in the
+    // own box -- carry samples, the others go in as adjacency-only entries.
+    const bool batch = P.blocks != nullptr;
+    int Z, Y, X;
+    int obz, oez, oby, oey, obx, oex;
+    int gbz, gez, gby, gey, gbx, gex;
+    uint32_t ntx, nty, tag = 0;
+    int64_t l_off = 0, d_off = 0;
+    if (batch) {
+        int lo = 0, hi = P.n_blocks;   // tile_prefix[lo] <= t < tile_prefix[hi]
+        while (hi - lo > 1) {
+            const int mid = (lo + hi) >> 1;
+            if (P.tile_prefix[mid] <= t) lo = mid;
+            else hi = mid;
+        }
+        const BlockGeom& G = P.blocks[lo];
+        t -= P.tile_prefix[lo];
+        Z = G.shape[0]; Y = G.shape[1]; X = G.shape[2];
+        obz = G.own_begin[0]; oez = G.own_end[0]; oby = G.own_begin[1]; oey = G.own_end[1];
+        obx = G.own_begin[2]; oex = G.own_end[2];
+        gbz = G.graph_begin[0]; gez = G.graph_end[0]; gby = G.graph_begin[1]; gey = G.graph_end[1];
+        gbx = G.graph_begin[2]; gex = G.graph_end[2];
+        ntx = (uint32_t)G.ntx;
+        nty = (uint32_t)G.nty;
+        l_off = G.label_offset;
+        d_off = G.data_offset;
+        tag = P.tag_shift < 32 ? (uint32_t)lo << P.tag_shift : 0u;
+    } else {
+        Z = (int)P.shape[0]; Y = (int)P.shape[1]; X = (int)P.shape[2];
+        obz = (int)P.own_begin[0]; oez = (int)P.own_end[0];
+        oby = (int)P.own_begin[1]; oey = (int)P.own_end[1];
+        obx = (int)P.own_begin[2]; oex = (int)P.own_end[2];
+        gbz = gez = gby = gey = gbx = gex = 0;
+        ntx = (uint32_t)P.ntiles[0];
+        nty = (uint32_t)P.ntiles[1];
+    }
+    const int64_t sz = (int64_t)Y * X;
+    const int tx = (int)(t % ntx);
+    const int ty = (int)((t / ntx) % nty);
+    const int tz = (int)(t / (ntx * nty));
     const int x0 = tx * TILE_X;
     const int x = x0 + lane;
     const int yw = ty * WG_ROWS + wave * ROWS;   // first row of this wave (uniform)
     const int z0 = tz * P.tile_z;
     const int z1 = min(z0 + P.tile_z, Z);
-    const LabelT* L = (const LabelT*)P.labels;
-    const DataT* D = (const DataT*)P.data;
+    const LabelT* L = (const LabelT*)P.labels + l_off;
+    const DataT* D = (const DataT*)P.data + d_off;
     const double scale = P.scale, offset = P.offset;
-    const int obz = (int)P.own_begin[0], oez = (int)P.own_end[0];
-    const int oby = (int)P.own_begin[1], oey = (int)P.own_end[1];
-    const int obx = (int)P.own_begin[2], oex = (int)P.own_end[2];
     const int ablate = P.ablate;
+    const uint32_t hi_mask = P.label_hi_mask;
     // lane masks (x is per lane): faces are owned by their upper voxel
     const bool inx = x < X;
     const bool own_x_lo = x >= obx && x < oex;
     const bool lane_xf = inx && x + 1 < X && x + 1 >= obx && x + 1 < oex;   // x face (x, x+1)
     const bool lane_yz = inx && own_x_lo;                                    // y / z faces, samples at p
+    // graph membership (batched): both voxels inside the graph box
+    const bool g_x_lo = batch && inx && x >= gbx && x < gex;
+    const bool glane_xf = g_x_lo && x + 1 < gex;
+    const bool glane_yz = g_x_lo;
     // row masks (uniform): bit r for row y = yw + r
-    uint32_t row_x = 0, row_y = 0;
+    uint32_t row_x = 0, row_y = 0, grow_x = 0, grow_y = 0;
 #pragma unroll
     for (int r = 0; r < ROWS; ++r) {
         const int y = yw + r;
         if (y < Y && y >= oby && y < oey) row_x |= 1u << r;
         if (y + 1 < Y && y + 1 >= oby && y + 1 < oey) row_y |= 1u << r;
+        if (batch && y < Y && y >= gby && y < gey) grow_x |= 1u << r;
+        if (batch && y + 1 < gey && y >= gby) grow_y |= 1u << r;
     }
-    const bool adj_marks = AFF && !P.skip_adj_marks;   // push nearest-neighbour adjacency markers
+    // adjacency markers of nearest-neighbour faces (affinities); batched
+    // blocks always push them (the block's sub-graph is the edge filter)
+    const bool adj_marks = AFF && (batch || !P.skip_adj_marks);
     const int xh = x0 + TILE_X;              // x of the lane-63 neighbour
     const bool has_xh = xh < X;
 
@@ -668,6 +614,7 @@ __global__ __launch_bounds__(SCAN_THREADS, 4) void k_face_scan(ScanParams P, Rec
 
     auto narrow = [&](LabelT l) -> uint32_t {
         if constexpr (sizeof(LabelT) == 8) ovf |= (uint32_t)(l >> 32);
+        ovf |= (uint32_t)l & hi_mask;   // batched blocks: the tag bits must be free
         return (uint32_t)l;
     };
     auto load_plane = [&](int z, LabelT (&Lb)[ROWS + 1], float (&Db)[ROWS + 1], LabelT& XL, float& XD) {
@@ -745,8 +692,8 @@ __global__ __launch_bounds__(SCAN_THREADS, 4) void k_face_scan(ScanParams P, Rec
         if (nbuf + k > STAGE_CAP) flush_stage();
         const int rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
         if (act) {
-            if constexpr (STATS) stage[nbuf + rank] = make_uint4(min(a, b), max(a, b), za, zb);
-            else stage[nbuf + rank] = make_uint2(min(a, b), max(a, b));
+            if constexpr (STATS) stage[nbuf + rank] = make_uint4(min(a, b) | tag, max(a, b), za, zb);
+            else stage[nbuf + rank] = make_uint2(min(a, b) | tag, max(a, b));
         }
         nbuf += k;
     };
@@ -762,6 +709,8 @@ __global__ __launch_bounds__(SCAN_THREADS, 4) void k_face_scan(ScanParams P, Rec
         if (hz) load_plane(z + 1, Ln, Dn, XLn, XDn);        // prefetch: in flight during x/y faces
         const bool zlo = z >= obz && z < oez;
         const bool zup = hz && z + 1 >= obz && z + 1 < oez;
+        const bool zg = batch && z >= gbz && z < gez;            // graph box planes (batched)
+        const bool gzup = zg && z + 1 < gez;
         if (ablate & 8) {   // diagnostic: loads only
             uint32_t chk = 0;
 #pragma unroll
@@ -773,17 +722,26 @@ __global__ __launch_bounds__(SCAN_THREADS, 4) void k_face_scan(ScanParams P, Rec
                 const uint32_t lc = Lc[r];
                 // x face (x, x+1); lane 63 takes its neighbour from the x-halo
                 const uint32_t lx = shl1(lc, (uint32_t)__builtin_amdgcn_readlane((int)XLc, r));
-                if (zlo && (row_x >> r & 1u) && (!AFF || adj_marks)) {
+                // owned faces carry samples; (batched) sub-graph faces the block
+                // does not own go in as adjacency-only entries
+                const bool xo = zlo && (row_x >> r & 1u), xg = zg && (grow_x >> r & 1u);
+                if ((xo || xg) && (!AFF || adj_marks)) {
                     const float dx = BND ? __uint_as_float(shl1(__float_as_uint(Dc[r]),
                                                                 (uint32_t)__builtin_amdgcn_readlane(
                                                                     (int)__float_as_uint(XDc), r)))
                                          : 0.f;
-                    push(lane_xf && lc != lx, lc, lx, __float_as_uint(Dc[r]), AFF ? MARK_ADJ : __float_as_uint(dx));
+                    const bool own = xo && lane_xf;
+                    push((own || (xg && glane_xf)) && lc != lx, lc, lx, own ? __float_as_uint(Dc[r]) : MARK_ADJ,
+                         (AFF || !own) ? MARK_ADJ : __float_as_uint(dx));
                 }
                 // y face (y, y+1)
-                if (zlo && (row_y >> r & 1u) && (!AFF || adj_marks))
-                    push(lane_yz && lc != Lc[r + 1], lc, Lc[r + 1], __float_as_uint(Dc[r]),
-                         AFF ? MARK_ADJ : __float_as_uint(Dc[r + 1]));
+                const bool yo = zlo && (row_y >> r & 1u), yg = zg && (grow_y >> r & 1u);
+                if ((yo || yg) && (!AFF || adj_marks)) {
+                    const bool own = yo && lane_yz;
+                    push((own || (yg && glane_yz)) && lc != Lc[r + 1], lc, Lc[r + 1],
+                         own ? __float_as_uint(Dc[r]) : MARK_ADJ,
+                         (AFF || !own) ? MARK_ADJ : __float_as_uint(Dc[r + 1]));
+                }
                 // affinity samples aff[c, p] for q = p + o_c, p in the owned box
                 if constexpr (AFF) {
                     const int y = yw + r;
@@ -846,13 +804,17 @@ __global__ __launch_bounds__(SCAN_THREADS, 4) void k_face_scan(ScanParams P, Rec
                 __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): the prefetched plane has landed
                 t_wait += stamp_now() - t0;
             }
-            if (zup && (!AFF || adj_marks)) {
+            if ((zup || gzup) && (!AFF || adj_marks)) {
 #pragma unroll
                 for (int r = 0; r < ROWS; ++r) {
                     const uint32_t ln = (uint32_t)Ln[r];
-                    if (row_x >> r & 1u)
-                        push(lane_yz && Lc[r] != ln, Lc[r], ln, __float_as_uint(Dc[r]),
-                             AFF ? MARK_ADJ : __float_as_uint(Dn[r]));
+                    const bool zo = zup && (row_x >> r & 1u), zgr = gzup && (grow_x >> r & 1u);
+                    if (zo || zgr) {
+                        const bool own = zo && lane_yz;
+                        push((own || (zgr && glane_yz)) && Lc[r] != ln, Lc[r], ln,
+                             own ? __float_as_uint(Dc[r]) : MARK_ADJ,
+                             (AFF || !own) ? MARK_ADJ : __float_as_uint(Dn[r]));
+                    }
                 }
             }
         }
@@ -899,10 +861,13 @@ __global__ __launch_bounds__(SCAN_THREADS, 4) void k_face_scan(ScanParams P, Rec
 template <typename LabelT, typename DataT, int MODE>
 static hipError_t launch_scan_t(const ScanParams& P, const RecordBuf& R, Counters* C, hipStream_t s) {
     ScanParams Q = P;
-    Q.ntiles[0] = (P.shape[2] + TILE_X - 1) / TILE_X;
-    Q.ntiles[1] = (P.shape[1] + WG_ROWS - 1) / WG_ROWS;
-    Q.ntiles[2] = (P.shape[0] + P.tile_z - 1) / P.tile_z;
-    const int64_t nwg = Q.ntiles[0] * Q.ntiles[1] * Q.ntiles[2];
+    int64_t nwg = P.batch_tiles;
+    if (!P.blocks) {
+        Q.ntiles[0] = (P.shape[2] + TILE_X - 1) / TILE_X;
+        Q.ntiles[1] = (P.shape[1] + WG_ROWS - 1) / WG_ROWS;
+        Q.ntiles[2] = (P.shape[0] + P.tile_z - 1) / P.tile_z;
+        nwg = Q.ntiles[0] * Q.ntiles[1] * Q.ntiles[2];
+    }
     if (nwg <= 0) return hipSuccess;
     if (nwg > 0x7FFFFFFF) return hipErrorInvalidValue;
     dim3 grid((unsigned)nwg);
@@ -1007,6 +972,109 @@ __global__ __launch_bounds__(UNIQ_THREADS) void k_unique_tiles(const uint64_t* L
         }
     }
 }
+
+// Per-block node lists of a batched call (ctg_rag_blocks): the unique labels
+// of every block's own box (its inner block, test_graph.py:53-60), one LDS set
+// per 64 x 8 x 16 tile, emitted as (block << 32) | label candidates; sorting
+// and de-duplicating them leaves each block's sorted nodes contiguous.
+template <typename LabelT>
+__global__ __launch_bounds__(UNIQ_THREADS) void k_unique_blocks(const LabelT* __restrict__ L,
+                                                                 const BlockGeom* __restrict__ blocks,
+                                                                 const uint32_t* __restrict__ tile_prefix,
+                                                                 int n_blocks, uint64_t* __restrict__ out,
+                                                                 unsigned long long* count, int64_t cap) {
+    __shared__ uint64_t set[USET_CAP];
+    __shared__ uint32_t used;
+    __shared__ unsigned long long base;
+    __shared__ uint32_t wpos;
+    const int tid = threadIdx.x;
+    for (int e = tid; e < USET_CAP; e += UNIQ_THREADS) set[e] = EMPTY_KEY;
+    if (tid == 0) used = 0;
+    uint32_t t = blockIdx.x;
+    int lo = 0, hi = n_blocks;
+    while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (tile_prefix[mid] <= t) lo = mid;
+        else hi = mid;
+    }
+    const BlockGeom& G = blocks[lo];
+    t -= tile_prefix[lo];
+    const int bz = G.own_begin[0], by = G.own_begin[1], bx = G.own_begin[2];
+    const int ez = G.own_end[0], ey = G.own_end[1], ex = G.own_end[2];
+    const uint32_t ntx = (uint32_t)(ex - bx + 63) / 64, nty = (uint32_t)(ey - by + TILE_Y - 1) / TILE_Y;
+    const int64_t Y = G.shape[1], X = G.shape[2];
+    const LabelT* Lb = L + G.label_offset;
+    const uint64_t tag = (uint64_t)lo << 32;
+    __syncthreads();
+    const int lane = tid & 63, wave = tid >> 6;
+    const int64_t x = bx + (int64_t)(t % ntx) * 64 + lane;
+    const int64_t y0 = by + (int64_t)((t / ntx) % nty) * TILE_Y;
+    const int64_t z0 = bz + (int64_t)(t / (ntx * nty)) * 16;
+    for (int zs = 0; zs < 16; zs += 4) {
+        const int64_t z = z0 + zs + wave;
+        if (z < ez) {
+            for (int dy = 0; dy < TILE_Y; ++dy) {
+                const int64_t y = y0 + dy;
+                if (y >= ey) break;
+                const uint64_t l = (x < ex) ? (tag | (uint32_t)Lb[(z * Y + y) * X + x]) : EMPTY_KEY;
+                uint32_t plo = __shfl_up((uint32_t)l, 1, 64), phi = __shfl_up((uint32_t)(l >> 32), 1, 64);
+                const uint64_t prev = ((uint64_t)phi << 32) | plo;
+                const bool head = (x < ex) && (lane == 0 || prev != l);
+                if (head) {
+                    uint32_t h = hash_key(l) & (USET_CAP - 1);
+                    for (int p = 0; p < USET_CAP; ++p) {
+                        const uint64_t cur = set[h];
+                        if (cur == l) break;
+                        if (cur == EMPTY_KEY) {
+                            const uint64_t old = atomicCAS((unsigned long long*)&set[h],
+                                                           (unsigned long long)EMPTY_KEY, (unsigned long long)l);
+                            if (old == EMPTY_KEY) {
+                                atomicAdd(&used, 1u);
+                                break;
+                            }
+                            if (old == l) break;
+                        }
+                        h = (h + 1) & (USET_CAP - 1);
+                    }
+                }
+            }
+        }
+        __syncthreads();
+        if (used > USET_CAP / 2 || zs + 4 >= 16) {
+            if (tid == 0) {
+                base = atomicAdd(count, (unsigned long long)used);
+                wpos = 0;
+            }
+            __syncthreads();
+            for (int e = tid; e < USET_CAP; e += UNIQ_THREADS) {
+                const uint64_t k = set[e];
+                if (k != EMPTY_KEY) {
+                    const uint32_t r = atomicAdd(&wpos, 1u);
+                    if (base + r < (unsigned long long)cap) out[base + r] = k;
+                    set[e] = EMPTY_KEY;
+                }
+            }
+            __syncthreads();
+            if (tid == 0) used = 0;
+            __syncthreads();
+        }
+    }
+}
+
+hipError_t launch_unique_blocks(const void* L, int label_bits, const BlockGeom* blocks, const uint32_t* tile_prefix,
+                                int n_blocks, int64_t n_tiles, uint64_t* out, unsigned long long* count, int64_t cap,
+                                hipStream_t s) {
+    if (n_tiles <= 0) return hipSuccess;
+    if (label_bits == 32)
+        hipLaunchKernelGGL(k_unique_blocks<uint32_t>, dim3((unsigned)n_tiles), dim3(UNIQ_THREADS), 0, s,
+                           (const uint32_t*)L, blocks, tile_prefix, n_blocks, out, count, cap);
+    else
+        hipLaunchKernelGGL(k_unique_blocks<uint64_t>, dim3((unsigned)n_tiles), dim3(UNIQ_THREADS), 0, s,
+                           (const uint64_t*)L, blocks, tile_prefix, n_blocks, out, count, cap);
+    return hipGetLastError();
+}
+
+int unique_tile_y() { return TILE_Y; }
 
 hipError_t launch_unique_tiles(const uint64_t* L, const int64_t* shape, const int64_t* b, const int64_t* e,
                                uint64_t* out, unsigned long long* count, int64_t cap, hipStream_t s) {

@@ -222,6 +222,123 @@ def rag_features(labels, data=None, offsets=None, own_begin=None, own_end=None, 
     return out
 
 
+class HostArena:
+    """Page-locked host buffer (ctg_host_alloc) viewed as a numpy array: the
+    staging area of batched block inputs (decoded N5 ROIs go straight in)."""
+
+    def __init__(self, nbytes):
+        self.nbytes = int(max(nbytes, 64))
+        lib = L.load()
+        L.init_device()
+        self.ptr = lib.ctg_host_alloc(self.nbytes)
+        if not self.ptr:
+            L.check(-3, 'ctg_host_alloc')
+        self.buf = (ctypes.c_char * self.nbytes).from_address(self.ptr)
+
+    def view(self, dtype, count, offset_bytes=0):
+        return np.frombuffer(self.buf, dtype=dtype, count=int(count), offset=int(offset_bytes))
+
+    def free(self):
+        if getattr(self, 'ptr', None):
+            L.load().ctg_host_free(self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        self.free()
+
+
+def _desc(blocks):
+    arr = (L.BlockDesc * len(blocks))()
+    for d, b in zip(arr, blocks):
+        d.label_offset = int(b['label_offset'])
+        d.data_offset = int(b.get('data_offset', 0))
+        for k in range(3):
+            d.shape[k] = int(b['shape'][k])
+            d.own_begin[k] = int(b['own'][0][k])
+            d.own_end[k] = int(b['own'][1][k])
+            d.graph_begin[k] = int(b['graph'][0][k])
+            d.graph_end[k] = int(b['graph'][1][k])
+    return arr
+
+
+def rag_blocks_arena(labels, blocks, data=None, offsets=None, ignore_label=False, hist_range=(0.0, 1.0),
+                     keep_stats=False):
+    """ctg_rag_blocks over arenas that already hold the block arrays.
+
+    labels: 1-D uint64/uint32 array (host, ideally a HostArena view);
+    data: None or 1-D float32/uint8 array; blocks: list of dicts with
+    label_offset, data_offset, shape, own=(begin, end), graph=(begin, end).
+    Returns one dict per block: nodes, edges[, features, sums, records]."""
+    lib = L.load()
+    dev = L.init_device()
+    labels = np.asarray(labels)
+    if labels.dtype not in (np.uint64, np.uint32):
+        raise ValueError('labels arena must be uint64 or uint32')
+    kind = L.CTG_DATA_NONE
+    n_ch = 0
+    off_ptr = None
+    if data is not None:
+        data = np.asarray(data)
+        kind = L.CTG_DATA_U8 if data.dtype == np.uint8 else L.CTG_DATA_F32
+        if kind == L.CTG_DATA_F32 and data.dtype != np.float32:
+            raise ValueError('data arena must be float32 or uint8')
+        if offsets is not None:
+            off = _check_offsets(offsets)
+            n_ch = off.shape[0]
+            off_ptr = off.ctypes.data_as(ctypes.c_void_p)
+    desc = _desc(blocks)
+    flags = L.CTG_KEEP_STATS if keep_stats else 0
+    h = ctypes.c_void_p()
+    rc = lib.ctg_rag_blocks(_ptr(labels), labels.dtype.itemsize * 8, _ptr(data), kind, n_ch, off_ptr,
+                            ctypes.cast(desc, ctypes.c_void_p), len(blocks), labels.size,
+                            0 if data is None else data.size, int(bool(ignore_label)), float(hist_range[0]),
+                            float(hist_range[1]), flags, L.CTG_MEM_HOST, None, ctypes.byref(h))
+    L.check(rc, 'ctg_rag_blocks')
+    r = Result(h, dev)
+    nb = len(blocks)
+    eoff = np.zeros(nb + 1, np.int64)
+    noff = np.zeros(nb + 1, np.int64)
+    L.check(lib.ctg_result_block_offsets(r.handle, _ptr(eoff), _ptr(noff)), 'ctg_result_block_offsets')
+    edges, nodes = r.edges(), r.nodes()
+    feats = r.features() if data is not None else None
+    sums = recs = None
+    if keep_stats and data is not None:
+        sums, recs = r.stats()
+    r.free()
+    out = []
+    for b in range(nb):
+        e0, e1, n0, n1 = eoff[b], eoff[b + 1], noff[b], noff[b + 1]
+        d = dict(edges=edges[e0:e1], nodes=nodes[n0:n1])
+        if feats is not None:
+            d['features'] = feats[e0:e1]
+        if sums is not None:
+            d['sums'], d['records'] = sums[e0:e1], recs[e0:e1]
+        out.append(d)
+    return out
+
+
+def rag_blocks(arrays, own, graph, data=None, offsets=None, ignore_label=False, hist_range=(0.0, 1.0),
+               keep_stats=False):
+    """Convenience front end of rag_blocks_arena: per-block label arrays
+    (and data arrays: (Z,Y,X) boundary maps or (C,Z,Y,X) affinities) with
+    their own / graph boxes ((begin, end) in array coordinates)."""
+    lab = [np.ascontiguousarray(np.asarray(a)) for a in arrays]
+    dt = np.uint32 if all(a.dtype == np.uint32 for a in lab) else np.uint64
+    lab_arena = np.concatenate([a.astype(dt, copy=False).ravel() for a in lab]) if lab else np.zeros(0, dt)
+    blocks, lo, do = [], 0, 0
+    dat_arena = None
+    if data is not None:
+        dd = [np.ascontiguousarray(np.asarray(x)) for x in data]
+        ddt = np.uint8 if all(x.dtype == np.uint8 for x in dd) else np.float32
+        dat_arena = np.concatenate([x.astype(ddt, copy=False).ravel() for x in dd])
+    for i, a in enumerate(lab):
+        blocks.append(dict(label_offset=lo, data_offset=do, shape=a.shape, own=own[i], graph=graph[i]))
+        lo += a.size
+        if data is not None:
+            do += data[i].size
+    return rag_blocks_arena(lab_arena, blocks, dat_arena, offsets, ignore_label, hist_range, keep_stats)
+
+
 def unique_labels(labels, begin=None, end=None):
     """Sorted unique labels of labels[begin:end] (uint64 numpy array)."""
     lib = L.load()

@@ -98,6 +98,45 @@ int ctg_rag_features(const void* labels, int label_bits,
                      int ignore_label, double hist_lo, double hist_hi,
                      int flags, int mem, void* stream, ctg_result** out);
 
+/*
+ * Batched per-block sub-graphs and features (the ndist per-block calls in
+ * one launch): block b is a C-order array of shape[b] starting at element
+ * label_offset[b] of `labels` (and data_offset[b] of `data`; affinities
+ * channel-first, C x shape).  For every block:
+ *   nodes    sorted unique labels of the own box (inner block,
+ *            test/graph/test_graph.py:53-60)
+ *   edges    sorted unique (u<v) keys of the faces with both voxels in the
+ *            graph box (increaseRoi: [begin-1, end), test_graph.py:42-84)
+ *   features (data != NULL) per edge, the 10 features of the samples owned by
+ *            the block -- boundary faces / affinity voxels whose upper voxel /
+ *            voxel p lies in the own box; edges of the graph box without owned
+ *            samples get count 0 (block_edge_features.py:127-145).  With
+ *            affinities a sample counts only if its pair is an edge of the
+ *            block's sub-graph.
+ * Rows [edge_off[b], edge_off[b+1]) of the edge / feature / stats tables and
+ * [node_off[b], node_off[b+1]) of the node table belong to block b
+ * (ctg_result_block_offsets).  Replaces the per-block loops of
+ * ndist.computeMergeableRegionGraph (graph/initial_sub_graphs.py:124-129) and
+ * ndist.extractBlockFeaturesFrom*Maps_* (features/block_edge_features.py:127-145).
+ */
+typedef struct ctg_block_desc {
+    int64_t label_offset;
+    int64_t data_offset;
+    int64_t shape[3];
+    int64_t own_begin[3], own_end[3];
+    int64_t graph_begin[3], graph_end[3];
+} ctg_block_desc;
+
+int ctg_rag_blocks(const void* labels, int label_bits, const void* data, int data_kind, int n_channels,
+                   const int32_t* offsets, const ctg_block_desc* blocks, int n_blocks, int64_t labels_len,
+                   int64_t data_len, int ignore_label, double hist_lo, double hist_hi, int flags, int mem,
+                   void* stream, ctg_result** out);
+int ctg_result_num_blocks(const ctg_result* r);
+/* page-locked host buffers for staging batched inputs (H2D at full PCIe rate) */
+void* ctg_host_alloc(int64_t bytes);
+void ctg_host_free(void* p);
+int ctg_result_block_offsets(const ctg_result* r, int64_t* edge_off, int64_t* node_off);
+
 /* sorted unique labels of labels[begin:end] (box in array coordinates) */
 int ctg_unique_labels(const uint64_t* labels, const int64_t* shape,
                       const int64_t* begin, const int64_t* end,
