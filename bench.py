@@ -15,6 +15,11 @@ them over RCCL (cluster_tools_amd/dist.py).
 
 The other BASELINE configs are extra lines (``--config``), not the driver's
 bench line:
+  0    configs[0]: the drop-in per-block path end to end -- GraphWorkflow +
+       EdgeFeaturesWorkflow job bodies (cluster_tools_amd/workflow.py) on a
+       125 x 1250 x 1250 volume in gzip N5 with 64 x 256 x 256 blocks, N5 in ->
+       N5 out; value = end-to-end Gvoxels/s, plus the compute-only rate of the
+       same per-block calls on device-resident inputs and the stage split
   2    configs[2]: 2048^3 boundary map (cell 16), strong scaling: the fixed
        volume is z-sharded over the ranks (2048/N planes each + 1 halo plane)
   3    configs[3]: 1024^3, 3-channel nearest-neighbour affinities (N=1)
@@ -41,6 +46,7 @@ EDGE_BYTES = 96                # 16 B (u,v) + 10 x float64 features (SURVEY 8(d)
 
 # BASELINE.json configs -> (cube edge, cell size, offsets or None, scaling, label)
 WORKLOADS = {
+    '0': (1250, 10, None, 'weak', 'BASELINE configs[0]: 125x%dx%d... per-block N5 workflow'),
     '1': (512, 10, None, 'weak', 'BASELINE configs[1]: %d^3 per GPU, cell %d, boundary map'),
     '2': (2048, 16, None, 'strong', 'BASELINE configs[2]: %d^3 boundary map, cell %d, z-slab sharded'),
     '3': (1024, 10, 'nn', 'strong', 'BASELINE configs[3]: %d^3, cell %d, 3-channel nearest-neighbour affinities'),
@@ -130,8 +136,118 @@ def cpu_baseline(labels_t, bnd_t, planes, workers):
         seconds=best, threads=workers)
 
 
+def bench_config0(args):
+    """BASELINE configs[0]: the per-block drop-in path, N5 in -> N5 out."""
+    import shutil
+    import tempfile
+    import torch
+    from cluster_tools_amd import _lib, n5, rag, workflow
+    from cluster_tools_amd.blocking import blocking
+    _lib.init_device(0 if args.device is None else args.device)
+    shape, block = (125, 1250, 1250), (64, 256, 256)
+    V = int(np.prod(shape))
+    lt, bt = rag.synth_volume(shape, cell=args.cell or 10, seed=args.seed)
+    lab = lt.cpu().numpy().view(np.uint64)
+    bnd = bt.cpu().numpy()
+    tmp_root = '/dev/shm' if os.path.isdir('/dev/shm') and shutil.disk_usage('/dev/shm').free > 12e9 else None
+    d = tempfile.mkdtemp(prefix='ctg_cfg0_', dir=tmp_root)
+    try:
+        inp = os.path.join(d, 'in.n5')
+        comp = {'type': 'gzip', 'level': 1, 'useZlib': False}
+        with n5.File(inp) as f:
+            for key, arr in (('seg', lab), ('bnd', bnd)):
+                ds = f.create_dataset(key, shape=shape, chunks=block, dtype=arr.dtype, compression=comp)
+                ds.n_threads = 16
+                ds[:] = arr
+        in_bytes = sum(os.path.getsize(os.path.join(r, fn)) for r, _, fs in os.walk(inp) for fn in fs)
+
+        def step(k):
+            out = os.path.join(d, 'out%d.n5' % k)
+            t = workflow.graph_workflow(inp, 'seg', out, 'graph', block, max_jobs=16)
+            workflow.edge_features_workflow(inp, 'bnd', inp, 'seg', out, 'graph', out, 'features', block,
+                                            max_jobs=1, max_jobs_merge=4, timer=t)
+            with n5.File(out, 'r') as f:
+                n_edges = int(f['graph'].attrs['numberOfEdges'])
+            shutil.rmtree(out)
+            return t.stages, n_edges
+
+        # a step is a whole workflow run (seconds): at most 1 warm-up + 3 steps
+        args.warmup, args.steps = min(args.warmup, 1), max(1, min(args.steps, 3))
+        for k in range(args.warmup):
+            step(k)
+        times, stages = [], {}
+        for k in range(args.steps):
+            t0 = time.perf_counter()
+            st, n_edges = step(100 + k)
+            times.append(time.perf_counter() - t0)
+            for key, v in st.items():
+                stages[key] = stages.get(key, 0.0) + v / args.steps
+        # compute only: the same per-block calls on device-resident inputs
+        blk = blocking([0, 0, 0], list(shape), list(block))
+        descs, lo = [], 0
+        arrays = []
+        for b in range(blk.numberOfBlocks):
+            bb = blk.getBlock(b)
+            rb = [max(x - 1, 0) for x in bb.begin]
+            sl = tuple(slice(x, y) for x, y in zip(rb, bb.end))
+            shp = [y - x for x, y in zip(rb, bb.end)]
+            descs.append(dict(label_offset=lo, data_offset=lo, shape=shp,
+                              own=([x - r for x, r in zip(bb.begin, rb)], [y - r for y, r in zip(bb.end, rb)]),
+                              graph=([0, 0, 0], shp)))
+            arrays.append(sl)
+            lo += int(np.prod(shp))
+        la = torch.cat([lt[sl].reshape(-1) for sl in arrays])
+        da = torch.cat([bt[sl].reshape(-1) for sl in arrays])
+        del lt, bt
+        rag.set_profiling(True)
+        for _ in range(2):
+            rag.rag_blocks_arena(la, descs)
+            rag.rag_blocks_arena(la, descs, da, keep_stats=True)
+        torch.cuda.synchronize()
+        c0 = time.perf_counter()
+        n_rep = 5
+        scan_ms = []
+        for _ in range(n_rep):
+            rag.rag_blocks_arena(la, descs)
+            rag.rag_blocks_arena(la, descs, da, keep_stats=True)
+            scan_ms.append(rag.last_timings()['scan'])
+        torch.cuda.synchronize()
+        compute_s = (time.perf_counter() - c0) / n_rep
+        rag.set_profiling(False)
+    finally:
+        shutil.rmtree(d, ignore_errors=True)
+    ms = float(np.mean(times)) * 1e3
+    scan_avg = float(np.mean(scan_ms))
+    alg = lo * 12                                   # the feature scan reads every block array (+ halo) once
+    line = {
+        'metric': 'Gvoxels/s RAG+edge features (per-block drop-in path, gzip N5 in -> N5 out, uint64 labels, '
+                  'float32 boundary map)',
+        'value': round(V / (ms * 1e-3) / 1e9, 4), 'unit': 'Gvoxels/s', 'n_gpus': 1, 'steps': args.steps,
+        'warmup': args.warmup, 'ms_per_step': round(ms, 2), 'higher_is_better': True, 'scaling': 'weak',
+        'vs_baseline': None, 'dtype': 'u64 labels / f32 samples / f64 stats',
+        'data': 'synthetic (jittered-grid Voronoi supervoxels + boundary map) written to gzip N5 (level 1)',
+        'config': {'workload': 'BASELINE configs[0]: 125x1250x1250, 64x256x256 blocks (50), GraphWorkflow + '
+                               'EdgeFeaturesWorkflow job bodies (16 graph jobs, 1 feature job, 4 merge jobs)',
+                   'volume': list(shape), 'block_shape': list(block), 'edges': n_edges,
+                   'input_n5_bytes': in_bytes},
+        'stage_s': {k: round(v, 4) for k, v in stages.items()},
+        'compute_only': {'value': round(V / compute_s / 1e9, 4), 'unit': 'Gvoxels/s',
+                         'ms': round(compute_s * 1e3, 3),
+                         'what': 'ctg_rag_blocks graph call + feature call over the 50 block arrays '
+                                 '(device-resident, halo planes included)'},
+        'roofline': {'bound': 'hbm', 'kernel': 'k_face_scan (batched blocks, features)',
+                     'kernel_ms': round(scan_avg, 4), 'algorithmic_bytes': alg,
+                     'achieved': round(alg / (scan_avg * 1e-3) / 1e9, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+                     'frac': round(alg / (scan_avg * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), 'traffic': None},
+        'cpu_baseline': None,
+    }
+    print(json.dumps(line), flush=True)
+
+
 def main():
     args = parse()
+    if args.config == '0':
+        return bench_config0(args)
     import torch
     import torch.distributed as dist
 

@@ -139,6 +139,16 @@ void ensure(void** p, size_t& have, size_t need) {
 
 static Workspace g_ws[64];
 Workspace& ws(int device) { return g_ws[device & 63]; }
+
+// One workspace per device: calls that use it are serialised per device, so
+// job threads may call the library concurrently (ctypes drops the GIL) --
+// their N5 decode overlaps, their GPU work queues.  Recursive: the dense
+// relabel and adjacency paths re-enter the C ABI.
+static std::recursive_mutex g_dev_mu[64];
+struct DevLock {
+    std::lock_guard<std::recursive_mutex> g;
+    DevLock() : g(g_dev_mu[cur_dev() & 63]) {}
+};
 int current_device() { return cur_dev(); }
 
 static hipError_t ws_init(Workspace& w) {
@@ -479,6 +489,7 @@ int ctg_device_count(int* count) {
 
 int ctg_init(int device) {
     int n = 0;
+    std::lock_guard<std::recursive_mutex> init_lock(g_dev_mu[device & 63]);
     CTG_CHECK(hipGetDeviceCount(&n));
     if (device < 0 || device >= n) {
         set_error("ctg_init: invalid device " + std::to_string(device));
@@ -490,6 +501,7 @@ int ctg_init(int device) {
 }
 
 int ctg_trim(void) {
+    DevLock dev_lock;
     // hand every cached device block of the current device back to HIP: the
     // workspace (records, sort scratch, staging) and the allocator's pool
     const int d = cur_dev();
@@ -671,6 +683,7 @@ int ctg_rag_features(const void* labels, int label_bits, const void* data, int d
                      const int32_t* offsets, const int64_t* shape, const int64_t* own_begin,
                      const int64_t* own_end, int ignore_label,
                      double hist_lo, double hist_hi, int flags, int mem, void* stream, ctg_result** out) {
+    DevLock dev_lock;
     if (!out || !shape || !labels) {
         set_error("ctg_rag_features: null argument");
         return CTG_ERR_ARG;
@@ -961,6 +974,7 @@ int ctg_rag_blocks(const void* labels, int label_bits, const void* data, int dat
                    const int32_t* offsets, const ctg_block_desc* blocks, int n_blocks, int64_t labels_len,
                    int64_t data_len, int ignore_label, double hist_lo, double hist_hi, int flags, int mem,
                    void* stream, ctg_result** out) {
+    DevLock dev_lock;
     if (!out || !labels || !blocks || n_blocks < 1 || n_blocks > (1 << 20) || labels_len < 0 ||
         (label_bits != 32 && label_bits != 64) || (data && data_kind != CTG_DATA_F32 && data_kind != CTG_DATA_U8) ||
         n_channels < 0 || n_channels > CTG_MAX_CHANNELS || (n_channels > 0 && !offsets) || !(hist_hi > hist_lo)) {
@@ -1175,6 +1189,16 @@ int ctg_rag_blocks(const void* labels, int label_bits, const void* data, int dat
         ctg_free(r);
         return rc;
     }
+    if (w.profiling && P.batch_tiles) {   // same phase split as ctg_rag_features ([5] = reduce end -> nodes)
+        CTG_CHECK(hipStreamSynchronize(s));
+        float ms = 0.f;
+        for (int i = 0; i < 6; ++i) {
+            hipEventElapsedTime(&ms, w.ev[i], w.ev[i + 1]);
+            w.last_ms[i] = ms;
+        }
+        hipEventElapsedTime(&ms, w.ev[0], w.ev[6]);
+        w.last_ms[6] = ms;
+    }
     *out = r;
     return CTG_OK;
 }
@@ -1211,6 +1235,7 @@ int ctg_result_block_offsets(const ctg_result* r, int64_t* edge_off, int64_t* no
 
 int ctg_unique_labels(const uint64_t* labels, const int64_t* shape, const int64_t* begin, const int64_t* end,
                       int mem, void* stream, ctg_result** out) {
+    DevLock dev_lock;
     if (!labels || !shape || !out) {
         set_error("ctg_unique_labels: null argument");
         return CTG_ERR_ARG;
@@ -1284,6 +1309,7 @@ int ctg_unique_labels(const uint64_t* labels, const int64_t* shape, const int64_
 }
 
 int ctg_unique_values(const uint64_t* values, int64_t n, int mem, void* stream, ctg_result** out) {
+    DevLock dev_lock;
     if (!out || n < 0 || (n > 0 && !values)) {
         set_error("ctg_unique_values: bad arguments");
         return CTG_ERR_ARG;
@@ -1333,6 +1359,7 @@ int ctg_unique_values(const uint64_t* values, int64_t n, int mem, void* stream, 
 
 int ctg_merge_stats(const uint64_t* keys, const double* sums, const uint32_t* records, int64_t n, double hist_lo,
                     double hist_hi, int keep_stats, int mem, void* stream, ctg_result** out) {
+    DevLock dev_lock;
     if (!out || n < 0 || (n > 0 && (!keys || !sums || !records))) {
         set_error("ctg_merge_stats: bad arguments");
         return CTG_ERR_ARG;
@@ -1414,6 +1441,7 @@ int ctg_merge_stats(const uint64_t* keys, const double* sums, const uint32_t* re
 
 int ctg_merge_feature_rows(const uint64_t* ids, const double* rows, int64_t n, int64_t id_begin, int64_t id_end,
                            double* out, int mem, void* stream) {
+    DevLock dev_lock;
     if (n < 0 || id_end < id_begin || (n > 0 && (!ids || !rows)) || (id_end > id_begin && !out)) {
         set_error("ctg_merge_feature_rows: bad arguments");
         return CTG_ERR_ARG;
@@ -1482,6 +1510,7 @@ int ctg_merge_feature_rows(const uint64_t* ids, const double* rows, int64_t n, i
 }
 
 int ctg_unique_pairs(const uint64_t* pairs, int64_t n, int mem, void* stream, ctg_result** out) {
+    DevLock dev_lock;
     if (!out || n < 0 || (n > 0 && !pairs)) {
         set_error("ctg_unique_pairs: bad arguments");
         return CTG_ERR_ARG;
@@ -1545,6 +1574,7 @@ int ctg_unique_pairs(const uint64_t* pairs, int64_t n, int mem, void* stream, ct
 
 int ctg_map_edge_ids(const uint64_t* global_edges, int64_t n_global, const uint64_t* query, int64_t n_query,
                      int64_t* out_ids, int mem, void* stream) {
+    DevLock dev_lock;
     if (n_global < 0 || n_query < 0 || (n_query > 0 && (!query || !out_ids))) {
         set_error("ctg_map_edge_ids: bad arguments");
         return CTG_ERR_ARG;

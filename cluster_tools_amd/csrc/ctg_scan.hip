@@ -485,7 +485,7 @@ __device__ __forceinline__ uint32_t shl1(uint32_t v, uint32_t edge) {
 #define FLUSH_TABLE table_flush
 #endif
 
-template <typename LabelT, typename DataT, int MODE, bool FAST40>
+template <typename LabelT, typename DataT, int MODE, bool FAST40, bool BATCH>
 __global__ __launch_bounds__(SCAN_THREADS, 4) void k_face_scan(ScanParams P, RecordBuf R, Counters* C) {
     constexpr bool BND = MODE == MODE_BOUNDARY;
     constexpr bool AFF = MODE == MODE_AFFINITY;
@@ -526,13 +526,13 @@ __global__ __launch_bounds__(SCAN_THREADS, 4) void k_face_scan(ScanParams P, Rec
     // whose tile range holds t.  Faces with both voxels in the graph box are
     // pushed (sub-graph edges); those owned by the block -- upper voxel in the
     // own box -- carry samples, the others go in as adjacency-only entries.
-    const bool batch = P.blocks != nullptr;
+    constexpr bool batch = BATCH;   // compile-time: the whole-array kernel carries none of this
     int Z, Y, X;
     int obz, oez, oby, oey, obx, oex;
     int gbz, gez, gby, gey, gbx, gex;
     uint32_t ntx, nty, tag = 0;
     int64_t l_off = 0, d_off = 0;
-    if (batch) {
+    if constexpr (BATCH) {
         int lo = 0, hi = P.n_blocks;   // tile_prefix[lo] <= t < tile_prefix[hi]
         while (hi - lo > 1) {
             const int mid = (lo + hi) >> 1;
@@ -573,7 +573,7 @@ __global__ __launch_bounds__(SCAN_THREADS, 4) void k_face_scan(ScanParams P, Rec
     const DataT* D = (const DataT*)P.data + d_off;
     const double scale = P.scale, offset = P.offset;
     const int ablate = P.ablate;
-    const uint32_t hi_mask = P.label_hi_mask;
+    const uint32_t hi_mask = BATCH ? P.label_hi_mask : 0u;
     // lane masks (x is per lane): faces are owned by their upper voxel
     const bool inx = x < X;
     const bool own_x_lo = x >= obx && x < oex;
@@ -614,7 +614,7 @@ __global__ __launch_bounds__(SCAN_THREADS, 4) void k_face_scan(ScanParams P, Rec
 
     auto narrow = [&](LabelT l) -> uint32_t {
         if constexpr (sizeof(LabelT) == 8) ovf |= (uint32_t)(l >> 32);
-        ovf |= (uint32_t)l & hi_mask;   // batched blocks: the tag bits must be free
+        if constexpr (BATCH) ovf |= (uint32_t)l & hi_mask;   // batched blocks: the tag bits must be free
         return (uint32_t)l;
     };
     auto load_plane = [&](int z, LabelT (&Lb)[ROWS + 1], float (&Db)[ROWS + 1], LabelT& XL, float& XD) {
@@ -692,8 +692,9 @@ __global__ __launch_bounds__(SCAN_THREADS, 4) void k_face_scan(ScanParams P, Rec
         if (nbuf + k > STAGE_CAP) flush_stage();
         const int rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
         if (act) {
-            if constexpr (STATS) stage[nbuf + rank] = make_uint4(min(a, b) | tag, max(a, b), za, zb);
-            else stage[nbuf + rank] = make_uint2(min(a, b) | tag, max(a, b));
+            const uint32_t lo_l = BATCH ? (min(a, b) | tag) : min(a, b);
+            if constexpr (STATS) stage[nbuf + rank] = make_uint4(lo_l, max(a, b), za, zb);
+            else stage[nbuf + rank] = make_uint2(lo_l, max(a, b));
         }
         nbuf += k;
     };
@@ -731,16 +732,16 @@ __global__ __launch_bounds__(SCAN_THREADS, 4) void k_face_scan(ScanParams P, Rec
                                                                     (int)__float_as_uint(XDc), r)))
                                          : 0.f;
                     const bool own = xo && lane_xf;
-                    push((own || (xg && glane_xf)) && lc != lx, lc, lx, own ? __float_as_uint(Dc[r]) : MARK_ADJ,
-                         (AFF || !own) ? MARK_ADJ : __float_as_uint(dx));
+                    push((own || (xg && glane_xf)) && lc != lx, lc, lx, (own || !BATCH) ? __float_as_uint(Dc[r]) : MARK_ADJ,
+                         (AFF || (BATCH && !own)) ? MARK_ADJ : __float_as_uint(dx));
                 }
                 // y face (y, y+1)
                 const bool yo = zlo && (row_y >> r & 1u), yg = zg && (grow_y >> r & 1u);
                 if ((yo || yg) && (!AFF || adj_marks)) {
                     const bool own = yo && lane_yz;
                     push((own || (yg && glane_yz)) && lc != Lc[r + 1], lc, Lc[r + 1],
-                         own ? __float_as_uint(Dc[r]) : MARK_ADJ,
-                         (AFF || !own) ? MARK_ADJ : __float_as_uint(Dc[r + 1]));
+                         (own || !BATCH) ? __float_as_uint(Dc[r]) : MARK_ADJ,
+                         (AFF || (BATCH && !own)) ? MARK_ADJ : __float_as_uint(Dc[r + 1]));
                 }
                 // affinity samples aff[c, p] for q = p + o_c, p in the owned box
                 if constexpr (AFF) {
@@ -812,8 +813,8 @@ __global__ __launch_bounds__(SCAN_THREADS, 4) void k_face_scan(ScanParams P, Rec
                     if (zo || zgr) {
                         const bool own = zo && lane_yz;
                         push((own || (zgr && glane_yz)) && Lc[r] != ln, Lc[r], ln,
-                             own ? __float_as_uint(Dc[r]) : MARK_ADJ,
-                             (AFF || !own) ? MARK_ADJ : __float_as_uint(Dn[r]));
+                             (own || !BATCH) ? __float_as_uint(Dc[r]) : MARK_ADJ,
+                             (AFF || (BATCH && !own)) ? MARK_ADJ : __float_as_uint(Dn[r]));
                     }
                 }
             }
@@ -871,10 +872,17 @@ static hipError_t launch_scan_t(const ScanParams& P, const RecordBuf& R, Counter
     if (nwg <= 0) return hipSuccess;
     if (nwg > 0x7FFFFFFF) return hipErrorInvalidValue;
     dim3 grid((unsigned)nwg);
-    if (P.fast40)
-        hipLaunchKernelGGL((k_face_scan<LabelT, DataT, MODE, true>), grid, dim3(SCAN_THREADS), 0, s, Q, R, C);
-    else
-        hipLaunchKernelGGL((k_face_scan<LabelT, DataT, MODE, false>), grid, dim3(SCAN_THREADS), 0, s, Q, R, C);
+    if (P.blocks) {
+        if (P.fast40)
+            hipLaunchKernelGGL((k_face_scan<LabelT, DataT, MODE, true, true>), grid, dim3(SCAN_THREADS), 0, s, Q, R, C);
+        else
+            hipLaunchKernelGGL((k_face_scan<LabelT, DataT, MODE, false, true>), grid, dim3(SCAN_THREADS), 0, s, Q, R,
+                               C);
+    } else if (P.fast40) {
+        hipLaunchKernelGGL((k_face_scan<LabelT, DataT, MODE, true, false>), grid, dim3(SCAN_THREADS), 0, s, Q, R, C);
+    } else {
+        hipLaunchKernelGGL((k_face_scan<LabelT, DataT, MODE, false, false>), grid, dim3(SCAN_THREADS), 0, s, Q, R, C);
+    }
     return hipGetLastError();
 }
 

@@ -204,14 +204,21 @@ class Dataset:
         lv = self.compression.get('level', 5)
         return 5 if lv is None or lv < 0 else int(lv)
 
-    def read_box_native(self, bb, n_threads=None):
-        """C-order box [(b, e), ...] through ctg_io_read_box, or None."""
+    def read_box_native(self, bb, n_threads=None, out=None):
+        """C-order box [(b, e), ...] through ctg_io_read_box (into ``out`` if
+        given: a C-contiguous native-endian array of the box's shape, e.g. a
+        view of a page-locked staging arena), or None without the library."""
         lib = _native()
         ct = self._ctype()
         if lib is None or ct is None:
             return None
         import ctypes
-        out = np.empty(tuple(e - b for b, e in bb), dtype=self.dtype.newbyteorder('='))
+        shape = tuple(e - b for b, e in bb)
+        if out is None:
+            out = np.empty(shape, dtype=self.dtype.newbyteorder('='))
+        elif tuple(out.shape) != shape or out.dtype != self.dtype.newbyteorder('=') or not out.flags.c_contiguous:
+            raise ValueError('read_box_native: out must be a C-contiguous %s array of shape %s'
+                             % (self.dtype, shape))
         rc = lib.ctg_io_read_box(self.path.encode(), self._FORMAT, self.dtype.itemsize, self._big_endian(),
                                  self.ndim, _i64(self.shape), _i64(self.chunks), ct, _i64([b for b, _ in bb]),
                                  _i64([e for _, e in bb]), out.ctypes.data_as(ctypes.c_void_p),

@@ -26,6 +26,8 @@ the reference's retry logic (cluster_tasks.py:114-159) applies unchanged.
 from __future__ import annotations
 
 import os
+import threading
+import time
 from concurrent.futures import ThreadPoolExecutor
 
 import numpy as np
@@ -82,39 +84,61 @@ def _subgraph_blocking(g):
 # graph
 # ---------------------------------------------------------------------------
 
+# seconds spent per phase by the last ndist call (read / compute / write);
+# bench.py reports the end-to-end split from it
+last_profile = {}
+_prof_lock = threading.Lock()
+
+
+def _prof(key, t0):
+    with _prof_lock:
+        last_profile[key] = last_profile.get(key, 0.0) + time.perf_counter() - t0
+    return time.perf_counter()
+
+
+IO_THREADS = int(os.environ.get('CTG_IO_THREADS', str(min(16, os.cpu_count() or 1))))
+
+
+def _read_into(ds, box, out, n_threads=None):
+    """ROI ``box`` [(b, e), ...] of ``ds`` into the C-contiguous array ``out``
+    (native threaded decode straight into the staging buffer when possible)."""
+    if ds.dtype.newbyteorder('=') == out.dtype and ds.read_box_native(box, n_threads=n_threads, out=out) is not None:
+        return
+    out[...] = ds[tuple(slice(b, e) for b, e in box)]
+
+
 def computeMergeableRegionGraph(labelsPath, labelsKey, roiBegin, roiEnd, graphPath,  # noqa: N802,N803
                                 subgraphKey, ignoreLabel, increaseRoi=True, serializeToVarlen=True):  # noqa: N803
     """Per-block sub-graph: sorted unique labels of the inner block (varlen
     ``nodes`` chunk) and the sorted unique (u<v) RAG edges of
     labels[max(begin-1,0):end] (varlen ``edges`` chunk, flattened; no chunk if
-    empty), semantics of test/graph/test_graph.py:42-84."""
+    empty), semantics of test_graph.py:42-84.  One ctg_rag_blocks call."""
     if not serializeToVarlen:
         raise NotImplementedError('computeMergeableRegionGraph only serializes to varlen chunks '
                                   '(the only mode the reference uses, initial_sub_graphs.py:129)')
+    last_profile.clear()
+    t = time.perf_counter()
     roiBegin = [int(b) for b in roiBegin]
     roiEnd = [int(e) for e in roiEnd]
     begin = [max(b - 1, 0) for b in roiBegin] if increaseRoi else list(roiBegin)
+    shape = [e - b for b, e in zip(begin, roiEnd)]
+    labels = np.empty(shape, dtype=np.uint64)
     with _open(labelsPath, 'r') as f:
-        labels = _roi(f[labelsKey], begin, roiEnd)
-    labels = np.ascontiguousarray(labels.astype(np.uint64, copy=False))
-    inner_b = [b - o for b, o in zip(roiBegin, begin)]
-    inner_e = [e - o for e, o in zip(roiEnd, begin)]
-    nodes = rag.unique_labels(labels, inner_b, inner_e)
-    edges = rag.rag_features(labels, None, ignore_label=bool(ignoreLabel))['edges']
+        _read_into(f[labelsKey], list(zip(begin, roiEnd)), labels)
+    t = _prof('read', t)
+    own = ([b - o for b, o in zip(roiBegin, begin)], [e - o for e, o in zip(roiEnd, begin)])
+    res = rag.rag_blocks_arena(labels.reshape(-1), [dict(label_offset=0, shape=shape, own=own,
+                                                         graph=([0, 0, 0], shape))],
+                               ignore_label=bool(ignoreLabel))[0]
+    t = _prof('compute', t)
     with _open(graphPath) as f:
         g = f[subgraphKey]
         ds_nodes = g['nodes']
         pos = [b // c for b, c in zip(roiBegin, ds_nodes.chunks)]
-        ds_nodes.write_chunk(pos, nodes, True)
-        if edges.shape[0]:
-            g['edges'].write_chunk(pos, edges.ravel(), True)
-
-
-def _read_block_graph(g, pos):
-    nodes = g['nodes'].read_chunk(pos)
-    edges = g['edges'].read_chunk(pos)
-    edges = None if edges is None else edges.reshape(-1, 2)
-    return nodes, edges
+        ds_nodes.write_chunk(pos, res['nodes'], True)
+        if res['edges'].shape[0]:
+            g['edges'].write_chunk(pos, res['edges'].ravel(), True)
+    _prof('write', t)
 
 
 def mergeSubgraphs(graphPath, subgraphKey, blockIds, outKey, numberOfThreads=1,  # noqa: N802,N803
@@ -127,9 +151,10 @@ def mergeSubgraphs(graphPath, subgraphKey, blockIds, outKey, numberOfThreads=1, 
         g = f[subgraphKey]
         blk, shape = _subgraph_blocking(g)
         block_ids = [int(b) for b in blockIds]
-        parts = _map(lambda b: _read_block_graph(g, blk.blockGridPosition(b)), block_ids, numberOfThreads)
-        node_list = [p[0] for p in parts if p[0] is not None and len(p[0])]
-        edge_list = [p[1] for p in parts if p[1] is not None and len(p[1])]
+        positions = [blk.blockGridPosition(b) for b in block_ids]
+        node_list = [n for n in g['nodes'].read_chunks(positions, numberOfThreads) if n is not None and len(n)]
+        edge_list = [e.reshape(-1, 2) for e in g['edges'].read_chunks(positions, numberOfThreads)
+                     if e is not None and len(e)]
         nodes = np.concatenate(node_list).astype(np.uint64) if node_list else np.zeros(0, np.uint64)
         if nodes.size:
             nodes = rag.unique_labels(nodes.reshape(1, 1, -1))
@@ -244,7 +269,7 @@ def mapEdgeIds(graphPath, graphKey, subgraphKey, blockIds, numberOfThreads=1):  
         g = f[subgraphKey]
         blk, _ = _subgraph_blocking(g)
         block_ids = [int(b) for b in blockIds]
-        chunks = _map(lambda b: g['edges'].read_chunk(blk.blockGridPosition(b)), block_ids, numberOfThreads)
+        chunks = g['edges'].read_chunks([blk.blockGridPosition(b) for b in block_ids], numberOfThreads)
         have = [(b, c.reshape(-1, 2)) for b, c in zip(block_ids, chunks) if c is not None and c.size]
         if not have:
             return
@@ -255,11 +280,12 @@ def mapEdgeIds(graphPath, graphKey, subgraphKey, blockIds, numberOfThreads=1):  
                                % int((ids < 0).sum()))
         ds = g['edge_ids']
         off = 0
-        writes = []
+        positions, datas = [], []
         for b, c in have:
-            writes.append((blk.blockGridPosition(b), ids[off:off + c.shape[0]].astype(np.uint64)))
+            positions.append(blk.blockGridPosition(b))
+            datas.append(ids[off:off + c.shape[0]].astype(np.uint64))
             off += c.shape[0]
-        _map(lambda w: ds.write_chunk(w[0], w[1], True), writes, numberOfThreads)
+        ds.write_chunks(positions, datas, varlen=True, n_threads=numberOfThreads)
 
 
 class Graph:
@@ -423,52 +449,134 @@ def _write_block_features(fo, outKey, pos, shape, chunks, feats, sums, records):
     _stats_dataset(fo, outKey, shape, chunks).write_chunk(pos, encode_stats_words(sums, records).ravel(), True)
 
 
+# bytes of decoded input (labels + data) staged per ctg_rag_blocks call
+BATCH_BYTES = int(os.environ.get('CTG_BLOCK_BATCH_BYTES', str(2 << 30)))
+
+
+def _batches(items, sizes, limit):
+    out, cur, acc = [], [], 0
+    for it, sz in zip(items, sizes):
+        if cur and acc + sz > limit:
+            out.append(cur)
+            cur, acc = [], 0
+        cur.append(it)
+        acc += sz
+    if cur:
+        out.append(cur)
+    return out
+
+
 def _block_features(graphPath, subgraphKey, dataPath, dataKey, labelsPath, labelsKey, blockIds,  # noqa: N803
-                    outPath, outKey, halo_lo, halo_hi, offsets, increaseRoi):  # noqa: N803
+                    outPath, outKey, halo_lo, halo_hi, offsets, increaseRoi, data_dtype):  # noqa: N803
+    """The job's blocks in batches of one ctg_rag_blocks call each: the ROIs
+    (block + halo) are decoded straight into a page-locked arena while the
+    previous batch runs on the GPU; per block the features of its stored
+    sub-graph edges (rows in the order of the ``edges`` chunk) and the
+    statistics companion are written as varlength chunks."""
+    last_profile.clear()
+    t = time.perf_counter()
     with _open(graphPath, 'r') as fg:
         g = fg[subgraphKey]
         blk, shape = _subgraph_blocking(g)
         ignore = bool(g.attrs.get('ignore_label', False))
-        ds_edges = g['edges']
         chunks = g['nodes'].chunks
-        with _open(dataPath, 'r') as fd, _open(labelsPath, 'r') as fl, _open(outPath) as fo:
-            ds_data = fd[dataKey]
-            ds_lab = fl[labelsKey]
-            for bid in [int(b) for b in blockIds]:
-                block = blk.getBlock(bid)
-                pos = blk.blockGridPosition(bid)
-                edges_b = ds_edges.read_chunk(pos)
-                if edges_b is None:
-                    continue
-                edges_b = edges_b.reshape(-1, 2)
-                lo = halo_lo if increaseRoi else [0, 0, 0]
-                rb = [max(b - h, 0) for b, h in zip(block.begin, lo)]
-                re_ = [min(e + h, s) for e, h, s in zip(block.end, halo_hi, shape)]
-                labels = np.ascontiguousarray(_roi(ds_lab, rb, re_).astype(np.uint64, copy=False))
-                if offsets is None:
-                    data = _roi(ds_data, rb, re_)
+        block_ids = [int(b) for b in blockIds]
+        stored = g['edges'].read_chunks([blk.blockGridPosition(b) for b in block_ids])
+    todo = [(b, e.reshape(-1, 2)) for b, e in zip(block_ids, stored) if e is not None]
+    t = _prof('read', t)
+    if not todo:
+        return
+    n_ch = 0 if offsets is None else len(offsets)
+    lo = halo_lo if increaseRoi else [0, 0, 0]
+    geo = []
+    for b, eb in todo:
+        block = blk.getBlock(b)
+        rb = [max(x - h, 0) for x, h in zip(block.begin, lo)]
+        re_ = [min(y + h, s_) for y, h, s_ in zip(block.end, halo_hi, shape)]
+        gb = [max(x - 1, 0) for x in block.begin] if increaseRoi else list(block.begin)
+        geo.append(dict(bid=b, edges=eb, rb=rb, re=re_, pos=blk.blockGridPosition(b),
+                        shape=[y - x for x, y in zip(rb, re_)],
+                        own=([x - r for x, r in zip(block.begin, rb)], [y - r for y, r in zip(block.end, rb)]),
+                        graph=([x - r for x, r in zip(gb, rb)], [y - r for y, r in zip(block.end, rb)])))
+    vox = [int(np.prod(x['shape'])) for x in geo]
+    per_voxel = 8 + max(1, n_ch) * data_dtype.itemsize
+    batches = _batches(list(range(len(geo))), [v * per_voxel for v in vox], BATCH_BYTES)
+    max_vox = max(sum(vox[i] for i in bt) for bt in batches)
+    arenas = [(rag.HostArena(max_vox * 8), rag.HostArena(max_vox * max(1, n_ch) * data_dtype.itemsize))
+              for _ in range(min(2, len(batches)))]
+
+    with _open(dataPath, 'r') as fd, _open(labelsPath, 'r') as fl, _open(outPath) as fo:
+        ds_data, ds_lab = fd[dataKey], fl[labelsKey]
+        ds_out = fo[outKey]
+        ds_st = _stats_dataset(fo, outKey, shape, chunks)
+
+        def load(k):
+            """decode batch k into arena k % 2 -> (label arena, data arena, descriptors)"""
+            la, da = arenas[k % 2]
+            descs, reads, lo_, do_ = [], [], 0, 0
+            for i in batches[k]:
+                x = geo[i]
+                v = vox[i]
+                box = list(zip(x['rb'], x['re']))
+                reads.append((ds_lab, box, la.view(np.uint64, v, lo_ * 8).reshape(x['shape'])))
+                if n_ch:
+                    dv = da.view(data_dtype, v * n_ch, do_ * data_dtype.itemsize).reshape([n_ch] + x['shape'])
+                    reads.append((ds_data, [(0, n_ch)] + box, dv))
                 else:
-                    data = ds_data[(slice(0, len(offsets)),) + tuple(slice(b, e) for b, e in zip(rb, re_))]
-                own_b = [b - r for b, r in zip(block.begin, rb)]
-                own_e = [e - r for e, r in zip(block.end, rb)]
-                # affinities: keep every sampled pair; the block's sub-graph edge
-                # list is the adjacency filter (map_edge_ids below), as in ndist
-                res = rag.rag_features(labels, data, offsets=offsets, own_begin=own_b, own_end=own_e,
-                                       ignore_label=ignore, keep_stats=True, no_adj_filter=offsets is not None)
-                rows = rag.map_edge_ids(res['edges'], edges_b) if res['edges'].shape[0] else \
-                    np.full(edges_b.shape[0], -1, np.int64)
-                hit = rows >= 0
-                feats = np.zeros((edges_b.shape[0], N_FEATURES), np.float64)
-                sums = np.zeros((edges_b.shape[0], 2), np.float64)
-                recs = np.zeros((edges_b.shape[0], rag.WIDE_WORDS), np.uint32)
-                # edges of the sub-graph without owned samples: empty records
-                # (ordered +inf min / -inf max are the identities of the merge)
-                recs[:, 43] = ORD_POS_INF
-                recs[:, 44] = ORD_NEG_INF
-                feats[hit] = res['features'][rows[hit]]
-                sums[hit] = res['sums'][rows[hit]]
-                recs[hit] = res['records'][rows[hit]]
-                _write_block_features(fo, outKey, pos, shape, chunks, feats, sums, recs)
+                    reads.append((ds_data, box, da.view(data_dtype, v, do_ * data_dtype.itemsize).reshape(x['shape'])))
+                descs.append(dict(label_offset=lo_, data_offset=do_, shape=x['shape'], own=x['own'],
+                                  graph=x['graph']))
+                lo_ += v
+                do_ += v * max(1, n_ch)
+            # every ROI of the batch decoded at once (each over its chunks)
+            list(io.map(lambda r: _read_into(r[0], r[1], r[2], 2), reads))
+            return la.view(np.uint64, lo_), da.view(data_dtype, do_), descs
+
+        def write(k, results):
+            pos, feats, words = [], [], []
+            for i, res in zip(batches[k], results):
+                x = geo[i]
+                eb = x['edges']
+                if np.array_equal(res['edges'], eb):
+                    f, sm, rc = res['features'], res['sums'], res['records']
+                else:   # stored sub-graph from elsewhere: rows follow the stored edges
+                    rows = rag.map_edge_ids(res['edges'], eb) if res['edges'].shape[0] else \
+                        np.full(eb.shape[0], -1, np.int64)
+                    hit = rows >= 0
+                    f = np.zeros((eb.shape[0], N_FEATURES))
+                    sm = np.zeros((eb.shape[0], 2))
+                    rc = np.zeros((eb.shape[0], rag.WIDE_WORDS), np.uint32)
+                    rc[:, 43] = ORD_POS_INF   # identities of the merge for edges without samples
+                    rc[:, 44] = ORD_NEG_INF
+                    f[hit], sm[hit], rc[hit] = res['features'][rows[hit]], res['sums'][rows[hit]], \
+                        res['records'][rows[hit]]
+                pos.append(x['pos'])
+                feats.append(f.ravel())
+                words.append(encode_stats_words(sm, rc).ravel())
+            ds_out.write_chunks(pos, feats, varlen=True)
+            ds_st.write_chunks(pos, words, varlen=True)
+
+        with ThreadPoolExecutor(1) as reader, ThreadPoolExecutor(1) as writer, \
+                ThreadPoolExecutor(max(1, IO_THREADS // 2)) as io:
+            nxt = reader.submit(load, 0)
+            pending = None
+            for k in range(len(batches)):
+                t = time.perf_counter()
+                la, da, descs = nxt.result()
+                _prof('read_wait', t)
+                if k + 1 < len(batches):   # arena (k+1) % 2 held batch k-1, whose GPU call has returned
+                    nxt = reader.submit(load, k + 1)
+                t = time.perf_counter()
+                results = rag.rag_blocks_arena(la, descs, da, offsets=offsets, ignore_label=ignore,
+                                               keep_stats=True)
+                t = _prof('compute', t)
+                if pending is not None:
+                    pending.result()
+                pending = writer.submit(write, k, results)
+            if pending is not None:
+                t = time.perf_counter()
+                pending.result()
+                _prof('write_wait', t)
 
 
 def extractBlockFeaturesFromBoundaryMaps_float32(graphPath, subgraphKey, dataPath, dataKey,  # noqa: N802,N803
@@ -478,12 +586,15 @@ def extractBlockFeaturesFromBoundaryMaps_float32(graphPath, subgraphKey, dataPat
     boundary map; every face counted once globally (owned by the block holding
     its upper voxel), both voxel values are samples."""
     _block_features(graphPath, subgraphKey, dataPath, dataKey, labelsPath, labelsKey, blockIds, outPath,
-                    outKey, [1, 1, 1], [0, 0, 0], None, increaseRoi)
+                    outKey, [1, 1, 1], [0, 0, 0], None, increaseRoi, np.dtype(np.float32))
 
 
-def extractBlockFeaturesFromBoundaryMaps_uint8(*args, **kw):  # noqa: N802
+def extractBlockFeaturesFromBoundaryMaps_uint8(graphPath, subgraphKey, dataPath, dataKey,  # noqa: N802,N803
+                                               labelsPath, labelsKey, blockIds, outPath, outKey,  # noqa: N803
+                                               increaseRoi=True):  # noqa: N803
     """uint8 boundary maps: samples are value/255 (SURVEY OPEN-7)."""
-    extractBlockFeaturesFromBoundaryMaps_float32(*args, **kw)
+    _block_features(graphPath, subgraphKey, dataPath, dataKey, labelsPath, labelsKey, blockIds, outPath,
+                    outKey, [1, 1, 1], [0, 0, 0], None, increaseRoi, np.dtype(np.uint8))
 
 
 def extractBlockFeaturesFromAffinityMaps_float32(graphPath, subgraphKey, dataPath, dataKey,  # noqa: N802,N803
@@ -496,11 +607,18 @@ def extractBlockFeaturesFromAffinityMaps_float32(graphPath, subgraphKey, dataPat
     halo_lo = [max(1, int(max(0, -off[:, a].min()))) for a in range(3)]
     halo_hi = [int(max(0, off[:, a].max())) for a in range(3)]
     _block_features(graphPath, subgraphKey, dataPath, dataKey, labelsPath, labelsKey, blockIds, outPath,
-                    outKey, halo_lo, halo_hi, off.tolist(), True)
+                    outKey, halo_lo, halo_hi, off.tolist(), True, np.dtype(np.float32))
 
 
-def extractBlockFeaturesFromAffinityMaps_uint8(*args, **kw):  # noqa: N802
-    extractBlockFeaturesFromAffinityMaps_float32(*args, **kw)
+def extractBlockFeaturesFromAffinityMaps_uint8(graphPath, subgraphKey, dataPath, dataKey,  # noqa: N802,N803
+                                               labelsPath, labelsKey, blockIds, outPath, outKey,  # noqa: N803
+                                               offsets):
+    """uint8 affinities: samples are value/255 (SURVEY OPEN-7)."""
+    off = np.asarray(offsets, dtype=np.int64).reshape(-1, 3)
+    halo_lo = [max(1, int(max(0, -off[:, a].min()))) for a in range(3)]
+    halo_hi = [int(max(0, off[:, a].max())) for a in range(3)]
+    _block_features(graphPath, subgraphKey, dataPath, dataKey, labelsPath, labelsKey, blockIds, outPath,
+                    outKey, halo_lo, halo_hi, off.tolist(), True, np.dtype(np.uint8))
 
 
 def mergeFeatureBlocks(graphPath, subgraphKey, featuresPath, featuresKey, outPath, outKey,  # noqa: N802,N803
@@ -527,22 +645,21 @@ def mergeFeatureBlocks(graphPath, subgraphKey, featuresPath, featuresKey, outPat
         ds_feat = ff[featuresKey + STATS_SUFFIX] if have_stats else ff[featuresKey]
         width = STATS_WORDS if have_stats else N_FEATURES
 
-        def load(b):
-            pos = blk.blockGridPosition(int(b))
-            ids = ds_ids.read_chunk(pos)
-            if ids is None:
-                return None
-            rows = ds_feat.read_chunk(pos)
-            if rows is None:
-                return None
+        block_ids = [int(b) for b in blockIds]
+        positions = [blk.blockGridPosition(b) for b in block_ids]
+        all_ids = ds_ids.read_chunks(positions, numberOfThreads)
+        all_rows = ds_feat.read_chunks(positions, numberOfThreads)
+        parts = []
+        for b, ids, rows in zip(block_ids, all_ids, all_rows):
+            if ids is None or rows is None:
+                continue
             rows = rows.reshape(-1, width)
             if rows.shape[0] != ids.shape[0]:
                 raise RuntimeError('mergeFeatureBlocks: block %d has %d edge ids but %d feature rows'
-                                   % (int(b), ids.shape[0], rows.shape[0]))
+                                   % (b, ids.shape[0], rows.shape[0]))
             sel = (ids >= begin) & (ids < end)
-            return ids[sel], rows[sel]
-
-        parts = [p for p in _map(load, blockIds, numberOfThreads) if p is not None and len(p[0])]
+            if sel.any():
+                parts.append((ids[sel], rows[sel]))
     out = np.zeros((end - begin, N_FEATURES), np.float64)
     if parts:
         ids = np.concatenate([p[0] for p in parts]).astype(np.uint64)

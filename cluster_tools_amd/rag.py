@@ -271,17 +271,36 @@ def rag_blocks_arena(labels, blocks, data=None, offsets=None, ignore_label=False
     Returns one dict per block: nodes, edges[, features, sums, records]."""
     lib = L.load()
     dev = L.init_device()
-    labels = np.asarray(labels)
-    if labels.dtype not in (np.uint64, np.uint32):
-        raise ValueError('labels arena must be uint64 or uint32')
+    on_dev = _is_torch(labels)
+    if on_dev:   # device-resident arenas (torch CUDA tensors, int64/int32 views of the labels)
+        import torch
+        assert labels.is_cuda and labels.is_contiguous() and labels.element_size() in (4, 8)
+        label_bits = labels.element_size() * 8
+        n_lab = labels.numel()
+        if data is not None:
+            assert _is_torch(data) and data.is_cuda and data.is_contiguous()
+            assert data.dtype in (torch.float32, torch.uint8)
+    else:
+        labels = np.asarray(labels)
+        if labels.dtype not in (np.uint64, np.uint32):
+            raise ValueError('labels arena must be uint64 or uint32')
+        label_bits = labels.dtype.itemsize * 8
+        n_lab = labels.size
     kind = L.CTG_DATA_NONE
     n_ch = 0
     off_ptr = None
+    n_dat = 0
     if data is not None:
-        data = np.asarray(data)
-        kind = L.CTG_DATA_U8 if data.dtype == np.uint8 else L.CTG_DATA_F32
-        if kind == L.CTG_DATA_F32 and data.dtype != np.float32:
-            raise ValueError('data arena must be float32 or uint8')
+        if on_dev:
+            import torch
+            kind = L.CTG_DATA_U8 if data.dtype == torch.uint8 else L.CTG_DATA_F32
+            n_dat = data.numel()
+        else:
+            data = np.asarray(data)
+            kind = L.CTG_DATA_U8 if data.dtype == np.uint8 else L.CTG_DATA_F32
+            if kind == L.CTG_DATA_F32 and data.dtype != np.float32:
+                raise ValueError('data arena must be float32 or uint8')
+            n_dat = data.size
         if offsets is not None:
             off = _check_offsets(offsets)
             n_ch = off.shape[0]
@@ -289,10 +308,11 @@ def rag_blocks_arena(labels, blocks, data=None, offsets=None, ignore_label=False
     desc = _desc(blocks)
     flags = L.CTG_KEEP_STATS if keep_stats else 0
     h = ctypes.c_void_p()
-    rc = lib.ctg_rag_blocks(_ptr(labels), labels.dtype.itemsize * 8, _ptr(data), kind, n_ch, off_ptr,
-                            ctypes.cast(desc, ctypes.c_void_p), len(blocks), labels.size,
-                            0 if data is None else data.size, int(bool(ignore_label)), float(hist_range[0]),
-                            float(hist_range[1]), flags, L.CTG_MEM_HOST, None, ctypes.byref(h))
+    rc = lib.ctg_rag_blocks(_ptr(labels), label_bits, _ptr(data), kind, n_ch, off_ptr,
+                            ctypes.cast(desc, ctypes.c_void_p), len(blocks), n_lab, n_dat,
+                            int(bool(ignore_label)), float(hist_range[0]), float(hist_range[1]), flags,
+                            L.CTG_MEM_DEVICE if on_dev else L.CTG_MEM_HOST, _current_stream(on_dev),
+                            ctypes.byref(h))
     L.check(rc, 'ctg_rag_blocks')
     r = Result(h, dev)
     nb = len(blocks)

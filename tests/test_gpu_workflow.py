@@ -1,0 +1,92 @@
+"""GraphWorkflow + EdgeFeaturesWorkflow end to end (cluster_tools_amd.workflow:
+the reference's job bodies on job threads, N5 in -> N5 out), against the
+whole-volume call: BASELINE configs[0] geometry (125 x 1250 x 1250 with
+64 x 256 x 256 blocks, SURVEY 8(d)'s offline substitute) and small volumes
+with boundary maps and affinities.
+
+The merged graph equals the whole-volume RAG bit for bit (test_graph.py:95-115),
+the merged features the whole-volume features (mean / var / min / max to
+1e-5, counts and quantiles exact: the block statistics merge their
+histograms), nodes = unique labels.
+"""
+import numpy as np
+import pytest
+
+from cluster_tools_amd import n5, rag, workflow
+from cluster_tools_amd import synthetic as S
+from oracle import rag_oracle as O
+
+from test_gpu_parity import check_features
+
+pytestmark = pytest.mark.gpu
+
+
+def _write_inputs(path, lab, data, block, level=1):
+    comp = {'type': 'gzip', 'level': level, 'useZlib': False}
+    with n5.File(path) as f:
+        ds = f.create_dataset('seg', shape=lab.shape, chunks=block, dtype='uint64', compression=comp)
+        ds.n_threads = 16
+        ds[:] = lab
+        ch = block if data.ndim == 3 else (data.shape[0],) + tuple(block)
+        ds = f.create_dataset('bnd', shape=data.shape, chunks=ch, dtype=data.dtype, compression=comp)
+        ds.n_threads = 16
+        ds[:] = data
+
+
+def _run(tmp_path, lab, data, block, offsets=None, max_jobs=4, max_jobs_merge=2):
+    inp = str(tmp_path / 'in.n5')
+    out = str(tmp_path / 'out.n5')
+    _write_inputs(inp, lab, data, block)
+    t = workflow.graph_workflow(inp, 'seg', out, 'graph', block, max_jobs=max_jobs)
+    workflow.edge_features_workflow(inp, 'bnd', inp, 'seg', out, 'graph', out, 'features', block,
+                                    max_jobs=max_jobs, max_jobs_merge=max_jobs_merge, offsets=offsets, timer=t)
+    with n5.File(out, 'r') as f:
+        g = f['graph']
+        edges, nodes, feats = g['edges'][:], g['nodes'][:], f['features'][:]
+        assert g.attrs['numberOfEdges'] == edges.shape[0] and g.attrs['numberOfNodes'] == nodes.shape[0]
+        assert list(g.attrs['shape']) == list(lab.shape)
+    return edges, nodes, feats, t
+
+
+@pytest.mark.parametrize('dtype', ['float32', 'uint8'])
+def test_workflow_boundary_small(gpu, tmp_path, dtype):
+    lab, bnd = S.generate((40, 70, 90), cell=6, seed=51)
+    data = bnd if dtype == 'float32' else np.round(bnd * 255).astype(np.uint8)
+    edges, nodes, feats, _ = _run(tmp_path, lab, data, (16, 32, 32))
+    e_ref, f_ref = O.boundary_features(lab, data)
+    np.testing.assert_array_equal(edges, e_ref)
+    np.testing.assert_array_equal(nodes, np.unique(lab))
+    check_features(feats, f_ref)
+
+
+def test_workflow_affinities_small(gpu, tmp_path):
+    lab, bnd = S.generate((36, 60, 64), cell=6, seed=52)
+    affs = S.affinities_from_boundary(bnd, S.NN_OFFSETS)
+    edges, nodes, feats, _ = _run(tmp_path, lab, affs, (12, 32, 32), offsets=S.NN_OFFSETS)
+    e_ref, f_ref = O.affinity_features(lab, affs, S.NN_OFFSETS)
+    np.testing.assert_array_equal(edges, e_ref)
+    check_features(feats, f_ref)
+
+
+@pytest.mark.timeout(400)
+def test_workflow_configs0_geometry(gpu, tmp_path):
+    """BASELINE configs[0]: 125 x 1250 x 1250, 64 x 256 x 256 blocks (50
+    blocks), N5 (gzip) in -> N5 out, against one whole-volume call."""
+    torch = pytest.importorskip('torch')
+    shape, block = (125, 1250, 1250), (64, 256, 256)
+    lt, bt = rag.synth_volume(shape, cell=10, seed=0)
+    whole = rag.rag_features_handle(lt, bt)
+    e_ref, f_ref = whole.edges(), whole.features()
+    whole.free()
+    lab = lt.cpu().numpy().view(np.uint64)
+    bnd = bt.cpu().numpy()
+    del lt, bt
+    torch.cuda.empty_cache()
+    edges, nodes, feats, t = _run(tmp_path, lab, bnd, block, max_jobs=16, max_jobs_merge=4)
+    np.testing.assert_array_equal(edges, e_ref)
+    np.testing.assert_array_equal(nodes, np.unique(lab))
+    np.testing.assert_array_equal(feats[:, 9], f_ref[:, 9])
+    np.testing.assert_array_equal(feats[:, [2, 8]], f_ref[:, [2, 8]])
+    np.testing.assert_allclose(feats[:, :2], f_ref[:, :2], rtol=1e-9, atol=1e-12)
+    np.testing.assert_array_equal(feats[:, 3:8], f_ref[:, 3:8])
+    print('configs[0] stages (s):', {k: round(v, 3) for k, v in t.stages.items()})
