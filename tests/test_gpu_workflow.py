@@ -90,3 +90,41 @@ def test_workflow_configs0_geometry(gpu, tmp_path):
     np.testing.assert_allclose(feats[:, :2], f_ref[:, :2], rtol=1e-9, atol=1e-12)
     np.testing.assert_array_equal(feats[:, 3:8], f_ref[:, 3:8])
     print('configs[0] stages (s):', {k: round(v, 3) for k, v in t.stages.items()})
+
+
+def test_rag_blocks_concurrent_threads_are_deterministic(gpu):
+    """Job threads share the library (calls are serialised per device): four
+    threads running batched affinity / boundary calls at once give the same
+    results as one thread, call after call."""
+    from concurrent.futures import ThreadPoolExecutor
+    lab, bnd = S.generate((36, 60, 64), cell=6, seed=53)
+    affs = S.affinities_from_boundary(bnd, S.NN_OFFSETS)
+    own = [((1, 1, 1), (13, 31, 33)), ((0, 0, 0), (12, 30, 32))]
+    graph = [((0, 0, 0), (13, 31, 33)), ((0, 0, 0), (12, 30, 32))]
+    arrays = [lab[11:24, 29:60, 31:64], lab[:12, :30, :32]]
+    data = [affs[:, 11:24, 29:60, 31:64], affs[:, :12, :30, :32]]
+
+    def run(i):
+        if i % 2:
+            return rag.rag_blocks(arrays, own, graph, data=[bnd[11:24, 29:60, 31:64], bnd[:12, :30, :32]])
+        return rag.rag_blocks(arrays, own, graph, data=data, offsets=S.NN_OFFSETS, keep_stats=True)
+    ref = [run(0), run(1)]
+    with ThreadPoolExecutor(4) as ex:
+        outs = list(ex.map(run, range(16)))
+    for i, o in enumerate(outs):
+        for a, b in zip(o, ref[i % 2]):
+            for k in a:
+                np.testing.assert_array_equal(a[k], b[k])
+
+
+@pytest.mark.parametrize('max_jobs', [1, 4])
+def test_workflow_affinities_repeatable(gpu, tmp_path, max_jobs):
+    lab, bnd = S.generate((36, 60, 64), cell=6, seed=52)
+    affs = S.affinities_from_boundary(bnd, S.NN_OFFSETS)
+    e_ref, f_ref = O.affinity_features(lab, affs, S.NN_OFFSETS)
+    for rep in range(3):
+        d = tmp_path / ('r%d' % rep)
+        d.mkdir()
+        edges, nodes, feats, _ = _run(d, lab, affs, (12, 32, 32), offsets=S.NN_OFFSETS, max_jobs=max_jobs)
+        np.testing.assert_array_equal(edges, e_ref)
+        check_features(feats, f_ref)
