@@ -21,6 +21,7 @@ CTG_DATA_F32 = 1
 CTG_DATA_U8 = 2
 CTG_KEEP_STATS = 1
 CTG_NO_ADJ_FILTER = 2
+CTG_NO_NODES = 4
 CTG_MAX_CHANNELS = 24
 CTG_N_FEATURES = 10
 CTG_NBINS = 40
@@ -84,6 +85,7 @@ PROTOTYPES = {
     'ctg_io_read_varlen': (ctypes.c_int, [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.c_int64, c_vp,
                                           ctypes.c_int, c_vp, c_vp, ctypes.c_int]),
     'ctg_io_free': (None, [c_vp]),
+    'ctg_io_cache_clear': (None, []),
     'ctg_io_write_chunks': (ctypes.c_int, [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                            ctypes.c_int64, c_vp, c_vp, c_vp, c_vp, ctypes.c_int, ctypes.c_int,
                                            ctypes.c_int, ctypes.c_int]),

@@ -1184,7 +1184,12 @@ int ctg_rag_blocks(const void* labels, int label_bits, const void* data, int dat
         ctg_free(r);
         return CTG_ERR_HIP;
     }
-    rc = block_nodes(w, dl, label_bits, dgeom, n_blocks, uprefix, own_voxels, s, r);
+    if (flags & CTG_NO_NODES) {
+        r->node_off.assign(n_blocks + 1, 0);
+        rc = CTG_OK;
+    } else {
+        rc = block_nodes(w, dl, label_bits, dgeom, n_blocks, uprefix, own_voxels, s, r);
+    }
     if (rc) {
         ctg_free(r);
         return rc;

@@ -15,10 +15,13 @@ namespace ctg {
 // fixed geometry of the face-scan tiles and the LDS edge table
 // ---------------------------------------------------------------------------
 constexpr int WAVE = 64;
-constexpr int SCAN_THREADS = 512;      // 8 waves per workgroup
+#ifndef CTG_SCAN_THREADS
+#define CTG_SCAN_THREADS 512
+#endif
+constexpr int SCAN_THREADS = CTG_SCAN_THREADS;   // 8 waves per workgroup (1024: 16 waves, one per CU)
 constexpr int TILE_X = 64;             // one wave row
 constexpr int TILE_Y = 8;
-constexpr int TABLE_CAP = 512;         // LDS edge-table entries (power of two)
+constexpr int TABLE_CAP = SCAN_THREADS;   // LDS edge-table entries (power of two; one per thread in a flush)
 constexpr int NBINS = 40;              // vigra UserRangeHistogram<40> (nifty default)
 constexpr int NSLOTS = NBINS + 2;      // left outliers, 40 bins, right outliers
 constexpr int HWORDS = 21;             // 42 u16 slots packed in 21 u32 words

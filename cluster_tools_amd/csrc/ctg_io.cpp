@@ -20,12 +20,17 @@
 #include <cerrno>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <future>
+#include <list>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <sys/stat.h>
 #include <thread>
 #include <unistd.h>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/ctg.h"
@@ -173,6 +178,185 @@ void parallel_for(int64_t n, int n_threads, F&& f) {
     for (auto& t : th) t.join();
 }
 
+// ---------------------------------------------------------------------------
+// decoded-chunk cache: a block ROI with its 1-voxel halo touches up to 8
+// chunks, 7 of them only for a plane or a line, and its neighbours read the
+// same chunks again.  Decoded chunks stay in a process-wide LRU (budget
+// CTG_IO_CACHE_MB, default 4096; 0 disables), so every chunk is inflated
+// once per pass whatever the block order; concurrent readers of one chunk
+// wait for the first one's decode.  An entry is reused only while the file's
+// size and mtime are unchanged, and native writes drop it.
+// ---------------------------------------------------------------------------
+struct Chunk {
+    int64_t dims[MAXD];
+    std::vector<unsigned char> data;   // native-endian elements, C order
+};
+using ChunkPtr = std::shared_ptr<const Chunk>;
+
+struct CacheEntry {
+    std::shared_future<ChunkPtr> fut;
+    bool ready = false;
+    int64_t mtime_ns = 0, fsize = -1;
+    size_t bytes = 0;
+    std::list<std::string>::iterator lru;
+};
+
+std::mutex g_cache_mu;
+std::unordered_map<std::string, CacheEntry> g_cache;
+std::list<std::string> g_lru;   // front = most recently used (ready entries only)
+size_t g_cache_bytes = 0;
+
+size_t cache_budget() {
+    static const size_t b = [] {
+        const char* e = getenv("CTG_IO_CACHE_MB");
+        return (size_t)(e ? std::max(0ll, atoll(e)) : 4096ll) << 20;
+    }();
+    return b;
+}
+
+bool file_stamp(const std::string& path, int64_t& mtime_ns, int64_t& size) {
+    struct stat st;
+    if (stat(path.c_str(), &st) != 0) return false;
+    mtime_ns = (int64_t)st.st_mtim.tv_sec * 1000000000ll + st.st_mtim.tv_nsec;
+    size = (int64_t)st.st_size;
+    return true;
+}
+
+void cache_drop(const std::string& path) {
+    std::lock_guard<std::mutex> g(g_cache_mu);
+    for (auto it = g_cache.begin(); it != g_cache.end();) {
+        if (it->first.compare(0, path.size(), path) == 0 && it->first.size() > path.size() &&
+            it->first[path.size()] == '|') {
+            if (it->second.ready) {
+                g_cache_bytes -= it->second.bytes;
+                g_lru.erase(it->second.lru);
+            }
+            it = g_cache.erase(it);
+        } else {
+            ++it;
+        }
+    }
+}
+
+// decode one chunk file (nullptr with *missing for an absent chunk)
+ChunkPtr decode_chunk(const std::string& path, int format, int ndim, const int64_t* chunks, int es, bool swap,
+                      int compression, bool* missing, std::string* err) {
+    std::vector<unsigned char> file;
+    *missing = false;
+    if (!read_file(path, file, *missing)) {
+        *err = "cannot read " + path;
+        return nullptr;
+    }
+    if (*missing) return nullptr;
+    auto c = std::make_shared<Chunk>();
+    size_t off = 0;
+    if (format == CTG_IO_N5) {
+        if (file.size() < 4) {
+            *err = "truncated chunk " + path;
+            return nullptr;
+        }
+        const uint16_t mode = be16(file.data()), nd = be16(file.data() + 2);
+        if (mode != 0 || nd != ndim || file.size() < 4 + 4 * (size_t)nd) {
+            *err = "not a default-mode chunk of this dataset: " + path;
+            return nullptr;
+        }
+        for (int a = 0; a < ndim; ++a) c->dims[ndim - 1 - a] = be32(file.data() + 4 + 4 * a);
+        off = 4 + 4 * (size_t)nd;
+    } else {
+        for (int a = 0; a < ndim; ++a) c->dims[a] = chunks[a];
+    }
+    size_t n_el = 1;
+    for (int a = 0; a < ndim; ++a) n_el *= (size_t)c->dims[a];
+    c->data.resize(n_el * es);
+    if (compression == CTG_IO_GZIP) {
+        if (!inflate_all(file.data() + off, file.size() - off, c->data.data(), c->data.size())) {
+            *err = "corrupt compressed chunk " + path;
+            return nullptr;
+        }
+        if (swap && es > 1) {
+            std::vector<unsigned char> tmp(c->data.size());
+            swap_copy(tmp.data(), c->data.data(), n_el, es, true);
+            c->data.swap(tmp);
+        }
+    } else {
+        if (file.size() - off < n_el * es) {
+            *err = "truncated raw chunk " + path;
+            return nullptr;
+        }
+        swap_copy(c->data.data(), file.data() + off, n_el, es, swap);
+    }
+    return c;
+}
+
+ChunkPtr get_chunk(const std::string& path, int format, int ndim, const int64_t* chunks, int es, bool swap,
+                   int compression, bool* missing, std::string* err) {
+    const size_t budget = cache_budget();
+    if (budget == 0) return decode_chunk(path, format, ndim, chunks, es, swap, compression, missing, err);
+    int64_t mt = 0, sz = -1;
+    if (!file_stamp(path, mt, sz)) {
+        *missing = errno == ENOENT;
+        if (!*missing) *err = "cannot stat " + path;
+        return nullptr;
+    }
+    const std::string key = path + "|" + std::to_string(es) + (swap ? "s" : "n") + std::to_string(compression);
+    std::promise<ChunkPtr> prom;
+    std::shared_future<ChunkPtr> wait_for;
+    {
+        std::lock_guard<std::mutex> g(g_cache_mu);
+        auto it = g_cache.find(key);
+        if (it != g_cache.end()) {
+            CacheEntry& e = it->second;
+            if (!e.ready) {
+                wait_for = e.fut;
+            } else if (e.mtime_ns == mt && e.fsize == sz) {
+                g_lru.splice(g_lru.begin(), g_lru, e.lru);
+                return e.fut.get();
+            } else {   // the file changed: decode again
+                g_cache_bytes -= e.bytes;
+                g_lru.erase(e.lru);
+                g_cache.erase(it);
+            }
+        }
+        if (!wait_for.valid()) {
+            CacheEntry e;
+            e.fut = prom.get_future().share();
+            e.mtime_ns = mt;
+            e.fsize = sz;
+            g_cache.emplace(key, e);
+        }
+    }
+    if (wait_for.valid()) {
+        ChunkPtr c = wait_for.get();
+        if (c) return c;
+        return decode_chunk(path, format, ndim, chunks, es, swap, compression, missing, err);
+    }
+    ChunkPtr c = decode_chunk(path, format, ndim, chunks, es, swap, compression, missing, err);
+    prom.set_value(c);
+    std::lock_guard<std::mutex> g(g_cache_mu);
+    auto it = g_cache.find(key);
+    if (it == g_cache.end()) return c;
+    if (!c) {
+        g_cache.erase(it);
+        return c;
+    }
+    CacheEntry& e = it->second;
+    e.ready = true;
+    e.bytes = c->data.size();
+    g_lru.push_front(key);
+    e.lru = g_lru.begin();
+    g_cache_bytes += e.bytes;
+    while (g_cache_bytes > budget && g_lru.size() > 1) {
+        const std::string victim = g_lru.back();
+        g_lru.pop_back();
+        auto v = g_cache.find(victim);
+        if (v != g_cache.end()) {
+            g_cache_bytes -= v->second.bytes;
+            g_cache.erase(v);
+        }
+    }
+    return c;
+}
+
 int check_geometry(int ndim, const int64_t* shape, const int64_t* chunks, int dtype_size) {
     if (ndim < 1 || ndim > MAXD || dtype_size < 1 || dtype_size > 16) return -1;
     for (int a = 0; a < ndim; ++a)
@@ -229,57 +413,22 @@ int ctg_io_read_box(const char* ds_path, int format, int dtype_size, int big_end
             lo[a] = std::max(begin[a], cb[a]);
             hi[a] = std::min(end[a], cb[a] + cs[a]);
         }
-        std::vector<unsigned char> file, raw;
         bool missing = false;
+        std::string msg;
         const std::string path = chunk_path(ds_path, format, ndim, pos);
-        const unsigned char* payload = nullptr;
-        size_t payload_n = 0;
-        int64_t dims[MAXD];   // stored extent of the chunk (C order)
-        if (!read_file(path, file, missing)) {
-            err.set("ctg_io_read_box: cannot read " + path);
+        const ChunkPtr chunk = get_chunk(path, format, ndim, chunks, es, swap, compression, &missing, &msg);
+        if (!chunk && !missing) {
+            err.set("ctg_io_read_box: " + msg);
             return;
         }
-        if (!missing) {
-            size_t off = 0;
-            if (format == CTG_IO_N5) {
-                if (file.size() < 4) {
-                    err.set("ctg_io_read_box: truncated chunk " + path);
-                    return;
-                }
-                const uint16_t mode = be16(file.data()), nd = be16(file.data() + 2);
-                if (mode != 0 || nd != ndim || file.size() < 4 + 4 * (size_t)nd) {
-                    err.set("ctg_io_read_box: not a default-mode chunk of this dataset: " + path);
-                    return;
-                }
-                for (int a = 0; a < ndim; ++a) dims[ndim - 1 - a] = be32(file.data() + 4 + 4 * a);
-                off = 4 + 4 * (size_t)nd;
-            } else {
-                for (int a = 0; a < ndim; ++a) dims[a] = chunks[a];
-            }
+        const int64_t* dims = chunk ? chunk->dims : nullptr;
+        if (chunk)
             for (int a = 0; a < ndim; ++a)
                 if (dims[a] < hi[a] - cb[a]) {
                     err.set("ctg_io_read_box: chunk smaller than its grid cell: " + path);
                     return;
                 }
-            size_t n_el = 1;
-            for (int a = 0; a < ndim; ++a) n_el *= (size_t)dims[a];
-            if (compression == CTG_IO_GZIP) {
-                raw.resize(n_el * es);
-                if (!inflate_all(file.data() + off, file.size() - off, raw.data(), raw.size())) {
-                    err.set("ctg_io_read_box: corrupt compressed chunk " + path);
-                    return;
-                }
-                payload = raw.data();
-            } else {
-                if (file.size() - off < n_el * es) {
-                    err.set("ctg_io_read_box: truncated raw chunk " + path);
-                    return;
-                }
-                payload = file.data() + off;
-            }
-            payload_n = n_el;
-        }
-        (void)payload_n;
+        const unsigned char* payload = chunk ? chunk->data.data() : nullptr;
         // scatter rows (last axis contiguous)
         const int L = ndim - 1;
         const int64_t row = hi[L] - lo[L];
@@ -295,7 +444,7 @@ int ctg_io_read_box(const char* ds_path, int format, int dtype_size, int big_end
                 s = s * (missing ? 1 : dims[a]) + (missing ? 0 : ci2);
             }
             if (missing) std::memset(dst0 + (size_t)o * es, 0, (size_t)row * es);
-            else swap_copy(dst0 + (size_t)o * es, payload + (size_t)s * es, (size_t)row, es, swap);
+            else std::memcpy(dst0 + (size_t)o * es, payload + (size_t)s * es, (size_t)row * es);
             int a = L - 1;
             for (; a >= 0; --a) {
                 if (++idx[a] < hi[a]) break;
@@ -379,6 +528,16 @@ int ctg_io_read_varlen(const char* ds_path, int dtype_size, int ndim, int64_t n_
 
 void ctg_io_free(void* p) { free(p); }
 
+void ctg_io_cache_clear(void) {
+    std::lock_guard<std::mutex> g(g_cache_mu);
+    for (auto it = g_cache.begin(); it != g_cache.end();) {
+        if (it->second.ready) it = g_cache.erase(it);
+        else ++it;
+    }
+    g_lru.clear();
+    g_cache_bytes = 0;
+}
+
 int ctg_io_write_chunks(const char* ds_path, int format, int dtype_size, int big_endian, int ndim, int64_t n_chunks,
                         const int64_t* positions, const int64_t* chunk_shapes, const void* const* data,
                         const int64_t* n_elements, int varlen, int compression, int level, int n_threads) {
@@ -413,6 +572,7 @@ int ctg_io_write_chunks(const char* ds_path, int format, int dtype_size, int big
             payload.swap(be);
         }
         const std::string path = chunk_path(ds_path, format, ndim, pos);
+        cache_drop(path);
         if (!write_file_atomic(path, hdr, payload)) err.set("ctg_io_write_chunks: cannot write " + path);
     });
     if (!err.msg.empty()) {

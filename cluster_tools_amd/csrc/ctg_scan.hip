@@ -109,23 +109,6 @@ __device__ __forceinline__ uint32_t home_bucket(uint32_t u, uint32_t v) {
     return h & (TABLE_CAP - 4);
 }
 
-// Two-choice buckets (CTG_TWO_CHOICE): a key whose home bucket is full goes to
-// the first empty slot of a second, independently hashed bucket, so a lookup
-// costs at most two bucket reads.  A linear walk from a full bucket (the
-// fallback) costs one dependent LDS round trip per slot, paid again by every
-// later sample of a displaced key -- the long-range affinity scan, with many
-// distinct keys per tile, spent most of its time there.
-#ifndef CTG_TWO_CHOICE
-#define CTG_TWO_CHOICE 1
-#endif
-__device__ __forceinline__ uint32_t alt_bucket(uint32_t u, uint32_t v) {
-    uint32_t h = (u * 0x85EBCA77u) ^ (v * 0xC2B2AE3Du + 0x27D4EB2Fu);
-    h ^= h >> 16;
-    h *= 0x7FEB352Du;
-    h ^= h >> 15;
-    return h & (TABLE_CAP - 4);
-}
-
 // Workgroup barrier that orders LDS only.  __syncthreads() also waits for every
 // outstanding global load (vmcnt(0)), which would drain the next plane's
 // prefetch at every flush decision; nothing in the scan needs global-memory
@@ -460,31 +443,8 @@ __device__ __forceinline__ void fold_batch(Table& T, const StageT* __restrict__ 
                         s = (int)h[i] + empty;
                     }
                 }
-                uint32_t hw = h[i];
-                int ew = empty;
-#if CTG_TWO_CHOICE
-                if (s < 0) {   // home bucket full (or a lost race): the second bucket
-                    const uint32_t h2 = alt_bucket(e[i].x, e[i].y);
-                    const uint4 c01 = *reinterpret_cast<const uint4*>(&T.key[h2]);
-                    const uint4 c23 = *reinterpret_cast<const uint4*>(&T.key[h2 + 2]);
-                    int empty2;
-                    s = bucket_match(c01, c23, h2, key, empty2);
-                    if (s < 0 && empty2 >= 0) {
-                        const uint64_t old = atomicCAS((unsigned long long*)&T.key[h2 + empty2],
-                                                       (unsigned long long)EMPTY_KEY, (unsigned long long)key);
-                        if (old == EMPTY_KEY) {
-                            if (atomicAdd(&T.used, 1u) + 1u > FILL_SOFT) need = true;
-                            s = (int)h2 + empty2;
-                        } else if (old == key) {
-                            s = (int)h2 + empty2;
-                        }
-                    }
-                    hw = h2;
-                    ew = empty2;
-                }
-#endif
                 if (s < 0) {
-                    s = table_insert(T, hw, ew, key);
+                    s = table_insert(T, h[i], empty, key);
                     need |= s < 0 || (s & INSERT_OVER) != 0;
                     s = s < 0 ? s : (s & (INSERT_OVER - 1));
                 }

@@ -171,6 +171,11 @@ class Dataset:
         self.compression = meta.get('compression', {'type': 'raw'})
         self.attrs = Attributes(path)
         self.n_threads = 1
+        # paintera / imglib2 label multisets (uint8 varlen chunks, attribute
+        # isLabelMultiset): read as their per-voxel argmax labels (uint64)
+        self.is_label_multiset = bool(meta.get('isLabelMultiset', False))
+        if self.is_label_multiset:
+            self.dtype = np.dtype('uint64')
 
     @property
     def ndim(self):
@@ -210,7 +215,7 @@ class Dataset:
         view of a page-locked staging arena), or None without the library."""
         lib = _native()
         ct = self._ctype()
-        if lib is None or ct is None:
+        if lib is None or ct is None or self.is_label_multiset:
             return None
         import ctypes
         shape = tuple(e - b for b, e in bb)
@@ -323,8 +328,37 @@ class Dataset:
             f.write(buf)
         os.replace(tmp, p)
 
+    def _read_multiset_chunk(self, pos):
+        """argmax labels of a label-multiset chunk, or None if missing.
+
+        Serialisation (imglib2 / paintera N5 label multisets, written by
+        elf.label_multiset.serialize_multiset, label_multisets/create_multiset.py:
+        123-131), all big-endian: int32 n = voxels of the chunk, n x int64
+        argmax label per voxel, n x int32 byte offset of the voxel's entry list,
+        then the entry lists (int32 length, length x (int64 id, int32 count)).
+        The graph only needs the argmax (test_graph.py:140-161 compares the
+        multiset graph with the graph of the argmax segmentation).  Parity
+        unpinned: neither elf nor a fixture of the format is available here."""
+        p = self._chunk_path(pos)
+        if not os.path.exists(p):
+            return None
+        with open(p, 'rb') as f:
+            buf = f.read()
+        mode, nd = struct.unpack_from('>HH', buf, 0)
+        off = 4 + 4 * nd + (4 if mode == 1 else 0)
+        ctype = self.compression.get('type', 'raw')
+        raw = _decompress(buf[off:]) if ctype == 'gzip' else buf[off:]
+        shape = self._chunk_shape(tuple(int(x) for x in pos))
+        n_vox = int(np.prod(shape))
+        (n,) = struct.unpack_from('>i', raw, 0)
+        if n != n_vox or len(raw) < 4 + 12 * n:
+            raise ValueError('label multiset chunk %s: %d argmax entries for a %s chunk' % (p, n, shape))
+        return np.frombuffer(raw, dtype='>i8', count=n, offset=4).astype(np.uint64).reshape(shape)
+
     def read_chunk(self, pos):
         """Chunk data (varlen chunks as 1-D arrays) or None if missing."""
+        if self.is_label_multiset:
+            return self._read_multiset_chunk(pos)
         p = self._chunk_path(pos)
         if not os.path.exists(p):
             return None

@@ -426,8 +426,10 @@ class Graph:
 # ---------------------------------------------------------------------------
 
 def _stats_dataset(fo, outKey, shape, chunks):  # noqa: N803
+    # the library's own companion format: gzip level 1 (4-5x faster to write
+    # than z5's default level 5, which the reference-layout datasets keep)
     return fo.require_dataset(outKey + STATS_SUFFIX, shape=shape, chunks=chunks, dtype='uint32',
-                              compression='gzip')
+                              compression={'type': 'gzip', 'level': 1, 'useZlib': False})
 
 
 def encode_stats_words(sums, records):
@@ -568,7 +570,7 @@ def _block_features(graphPath, subgraphKey, dataPath, dataKey, labelsPath, label
                     nxt = reader.submit(load, k + 1)
                 t = time.perf_counter()
                 results = rag.rag_blocks_arena(la, descs, da, offsets=offsets, ignore_label=ignore,
-                                               keep_stats=True)
+                                               keep_stats=True, nodes=False)
                 t = _prof('compute', t)
                 if pending is not None:
                     pending.result()

@@ -262,7 +262,7 @@ def _desc(blocks):
 
 
 def rag_blocks_arena(labels, blocks, data=None, offsets=None, ignore_label=False, hist_range=(0.0, 1.0),
-                     keep_stats=False):
+                     keep_stats=False, nodes=True):
     """ctg_rag_blocks over arenas that already hold the block arrays.
 
     labels: 1-D uint64/uint32 array (host, ideally a HostArena view);
@@ -306,7 +306,7 @@ def rag_blocks_arena(labels, blocks, data=None, offsets=None, ignore_label=False
             n_ch = off.shape[0]
             off_ptr = off.ctypes.data_as(ctypes.c_void_p)
     desc = _desc(blocks)
-    flags = L.CTG_KEEP_STATS if keep_stats else 0
+    flags = (L.CTG_KEEP_STATS if keep_stats else 0) | (0 if nodes else L.CTG_NO_NODES)
     h = ctypes.c_void_p()
     rc = lib.ctg_rag_blocks(_ptr(labels), label_bits, _ptr(data), kind, n_ch, off_ptr,
                             ctypes.cast(desc, ctypes.c_void_p), len(blocks), n_lab, n_dat,

@@ -58,6 +58,7 @@ extern "C" {
 
 /* ctg_rag_features flags */
 #define CTG_KEEP_STATS 1      /* keep mergeable per-edge statistics (ctg_result_copy_stats) */
+#define CTG_NO_NODES 4        /* ctg_rag_blocks: skip the per-block node lists */
 #define CTG_NO_ADJ_FILTER 2   /* affinities: keep sample pairs that are not nearest-neighbour
                                  edges of this array (their records carry no ADJ bit); the
                                  caller filters after a merge or by an edge list */
@@ -216,6 +217,9 @@ int ctg_io_read_box(const char* ds_path, int format, int dtype_size, int big_end
 int ctg_io_read_varlen(const char* ds_path, int dtype_size, int ndim, int64_t n_chunks, const int64_t* positions,
                        int compression, void** out, int64_t* n_out, int n_threads);
 void ctg_io_free(void* p);
+/* drop the decoded-chunk cache of ctg_io_read_box (budget: env CTG_IO_CACHE_MB,
+ * default 4096; an entry is reused only while its file is unchanged) */
+void ctg_io_cache_clear(void);
 /* write n_chunks chunks (default mode with chunk_shapes, or N5 varlength) */
 int ctg_io_write_chunks(const char* ds_path, int format, int dtype_size, int big_endian, int ndim, int64_t n_chunks,
                         const int64_t* positions, const int64_t* chunk_shapes, const void* const* data,

@@ -325,3 +325,29 @@ def test_zarr_input_container(gpu, tmp_path):
                 assert got is None
             else:
                 np.testing.assert_array_equal(got.reshape(-1, 2), ref)
+
+
+def test_graph_on_label_multiset_input(gpu, tmp_path):
+    """test_graph.py:140-161: GraphWorkflow on a label-multiset dataset gives
+    the graph of its argmax segmentation (per-block nodes / edges and the
+    merged graph)."""
+    from test_host import write_multiset_dataset
+    lab, _ = S.generate(SHAPE, cell=5, seed=38, with_boundary=False)
+    p = _setup(tmp_path, lab)
+    with n5.File(p) as f:
+        write_multiset_dataset(f, 'ms', lab, BLOCK)
+    blk = blocking([0, 0, 0], list(SHAPE), list(BLOCK))
+    ids = list(range(blk.numberOfBlocks))
+    for b in ids:
+        bb = blk.getBlock(b)
+        ndist.computeMergeableRegionGraph(p, 'ms', bb.begin, bb.end, p, 's0/sub_graphs', False,
+                                          increaseRoi=True, serializeToVarlen=True)
+    ndist.mergeSubgraphs(p, subgraphKey='s0/sub_graphs', blockIds=ids, outKey='graph', numberOfThreads=2)
+    with n5.File(p, 'r') as f:
+        g = f['s0/sub_graphs']
+        for b in ids:
+            bb = blk.getBlock(b)
+            pos = blk.blockGridPosition(b)
+            np.testing.assert_array_equal(g['nodes'].read_chunk(pos),
+                                          np.unique(lab[tuple(slice(x, y) for x, y in zip(bb.begin, bb.end))]))
+    np.testing.assert_array_equal(ndist.Graph(p, 'graph').uvIds(), O.rag_edges(lab))

@@ -353,3 +353,70 @@ def test_native_varlen_batches(tmp_path, monkeypatch):
         f.create_dataset('d', data=np.ones((4, 4, 4), np.uint64), chunks=(2, 2, 2))
         with pytest.raises(OSError):
             f['d'].read_chunks([(0, 0, 0)])
+
+
+def test_native_chunk_cache_sees_rewrites_and_threads(tmp_path, monkeypatch):
+    """ctg_io_read_box's decoded-chunk cache: re-reads after a native or a
+    Python rewrite of a chunk return the new data; concurrent overlapping
+    reads (the halo of neighbouring blocks) agree."""
+    from concurrent.futures import ThreadPoolExecutor
+    _with_codec(monkeypatch, True)
+    p = str(tmp_path / 'c.n5')
+    rng = np.random.default_rng(4)
+    data = rng.integers(0, 2 ** 40, (24, 40, 40), dtype=np.uint64)
+    with n5.File(p) as f:
+        ds = f.create_dataset('d', shape=data.shape, chunks=(8, 16, 16), dtype='uint64', compression='gzip')
+        ds[:] = data
+        np.testing.assert_array_equal(ds[:], data)
+        boxes = [(slice(max(z - 1, 0), z + 8), slice(max(y - 1, 0), y + 16), slice(max(x - 1, 0), x + 16))
+                 for z in range(0, 24, 8) for y in range(0, 40, 16) for x in range(0, 40, 16)]
+        with ThreadPoolExecutor(8) as ex:
+            outs = list(ex.map(lambda b: ds[b], boxes * 3))
+        for b, o in zip(boxes * 3, outs):
+            np.testing.assert_array_equal(o, data[b])
+        new = data[:8, :16, :16] + np.uint64(7)
+        ds.write_chunks([(0, 0, 0)], [new])                       # native write drops the entry
+        np.testing.assert_array_equal(ds[:8, :16, :16], new)
+        _with_codec(monkeypatch, False)
+        ds.write_chunk((0, 0, 0), new + np.uint64(1))             # python write: the file stamp changes
+        _with_codec(monkeypatch, True)
+        np.testing.assert_array_equal(ds[:8, :16, :16], new + np.uint64(1))
+    n5._native().ctg_io_cache_clear()
+
+
+def serialize_argmax_multiset(labels):
+    """A label multiset of one label per voxel in the imglib2 / paintera N5
+    serialisation (test-side writer, the restated format of n5.Dataset.
+    _read_multiset_chunk): int32 n, n x int64 argmax, n x int32 list offsets,
+    lists (int32 size, size x (int64 id, int32 count)), big-endian."""
+    flat = np.asarray(labels, dtype=np.uint64).ravel()
+    uniq, inv = np.unique(flat, return_inverse=True)
+    lists = b''.join(struct.pack('>iqi', 1, int(u), 1) for u in uniq)
+    offsets = (inv * 16).astype('>i4')
+    head = struct.pack('>i', flat.size)
+    return np.frombuffer(head + flat.astype('>i8').tobytes() + offsets.tobytes() + lists, dtype=np.uint8)
+
+
+def write_multiset_dataset(group, key, labels, chunks):
+    ds = group.create_dataset(key, shape=labels.shape, chunks=chunks, dtype='uint8', compression='gzip')
+    ds.attrs['isLabelMultiset'] = True
+    ds.attrs['maxId'] = int(labels.max())
+    blk = B.blocking([0, 0, 0], list(labels.shape), list(chunks))
+    for b in range(blk.numberOfBlocks):
+        bb = blk.getBlock(b)
+        sl = tuple(slice(x, y) for x, y in zip(bb.begin, bb.end))
+        if labels[sl].sum() == 0:      # create_multiset.py:118-121 skips empty blocks
+            continue
+        ds.write_chunk(blk.blockGridPosition(b), serialize_argmax_multiset(labels[sl]), True)
+
+
+def test_label_multiset_reads_as_argmax(tmp_path):
+    lab, _ = S.generate((20, 30, 26), cell=5, seed=12, with_boundary=False)
+    lab[:8, :10, :10] = 0                                    # an empty (unwritten) chunk
+    with n5.File(str(tmp_path / 'm.n5')) as f:
+        write_multiset_dataset(f, 'ms', lab, (8, 10, 10))
+    with n5.File(str(tmp_path / 'm.n5'), 'r') as f:
+        ds = f['ms']
+        assert ds.is_label_multiset and ds.dtype == np.uint64
+        np.testing.assert_array_equal(ds[:], lab)
+        np.testing.assert_array_equal(ds[3:17, 4:29, 1:25], lab[3:17, 4:29, 1:25])
