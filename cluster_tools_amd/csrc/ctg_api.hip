@@ -240,11 +240,8 @@ using RecordSortConfig = rocprim::default_config;
 // 14.1 -> 18.7 ms, the 1024-way scatter coalesces worse), so they are used up
 // to this many records (CTG_SORT_WIDE_MAX overrides).
 static bool sort_packed() {
-    static const bool v = [] {
-        const char* e = getenv("CTG_SORT_PACKED");
-        return !(e && e[0] == '0');
-    }();
-    return v;
+    const char* e = getenv("CTG_SORT_PACKED");   // read per call: tests switch it
+    return !(e && e[0] == '0');
 }
 static int64_t sort_wide_digits_max() {
     static const int64_t v = [] {

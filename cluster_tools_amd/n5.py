@@ -504,6 +504,7 @@ class ZarrArray(Dataset):
         self.sep = meta.get('dimension_separator', '.')
         self.attrs = Attributes(path, _ZATTRS)
         self.n_threads = 1
+        self.is_label_multiset = False
 
     @property
     def _FORMAT(self):  # noqa: N802

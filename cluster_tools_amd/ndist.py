@@ -504,8 +504,19 @@ def _block_features(graphPath, subgraphKey, dataPath, dataKey, labelsPath, label
     per_voxel = 8 + max(1, n_ch) * data_dtype.itemsize
     batches = _batches(list(range(len(geo))), [v * per_voxel for v in vox], BATCH_BYTES)
     max_vox = max(sum(vox[i] for i in bt) for bt in batches)
-    arenas = [(rag.HostArena(max_vox * 8), rag.HostArena(max_vox * max(1, n_ch) * data_dtype.itemsize))
+    arenas = [(rag.host_arena(max_vox * 8), rag.host_arena(max_vox * max(1, n_ch) * data_dtype.itemsize))
               for _ in range(min(2, len(batches)))]
+    try:
+        _block_batches(batches, arenas, geo, vox, n_ch, data_dtype, dataPath, dataKey, labelsPath, labelsKey,
+                       outPath, outKey, shape, chunks, offsets, ignore)
+    finally:
+        for pair in arenas:
+            for a in pair:
+                rag.release_arena(a)
+
+
+def _block_batches(batches, arenas, geo, vox, n_ch, data_dtype, dataPath, dataKey, labelsPath, labelsKey,  # noqa: N803
+                   outPath, outKey, shape, chunks, offsets, ignore):  # noqa: N803
 
     with _open(dataPath, 'r') as fd, _open(labelsPath, 'r') as fl, _open(outPath) as fo:
         ds_data, ds_lab = fd[dataKey], fl[labelsKey]

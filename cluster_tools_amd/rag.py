@@ -8,6 +8,7 @@ calls after reading blocks from N5.
 from __future__ import annotations
 
 import ctypes
+import threading
 
 import numpy as np
 
@@ -220,6 +221,34 @@ def rag_features(labels, data=None, offsets=None, own_begin=None, own_end=None, 
     out['n_records'], out['n_direct'] = r.info()
     r.free()
     return out
+
+
+_arena_pool = []
+_arena_lock = threading.Lock()
+ARENA_POOL_BYTES = 8 << 30
+
+
+def host_arena(nbytes):
+    """A page-locked arena of at least ``nbytes`` from the process pool
+    (pinning GBs of host memory costs ~0.2 s/GB: arenas are kept for the next
+    batch / call); give it back with release_arena."""
+    with _arena_lock:
+        best = None
+        for a in _arena_pool:
+            if a.nbytes >= nbytes and (best is None or a.nbytes < best.nbytes):
+                best = a
+        if best is not None:
+            _arena_pool.remove(best)
+            return best
+    return HostArena(nbytes)
+
+
+def release_arena(arena):
+    with _arena_lock:
+        _arena_pool.append(arena)
+        _arena_pool.sort(key=lambda a: -a.nbytes)
+        while sum(a.nbytes for a in _arena_pool) > ARENA_POOL_BYTES and len(_arena_pool) > 1:
+            _arena_pool.pop().free()
 
 
 class HostArena:

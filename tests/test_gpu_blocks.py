@@ -127,3 +127,16 @@ def test_blocks_empty_and_uniform_blocks(gpu):
     res = rag.rag_blocks([lab[g['roi']] for g in geo], [g['own'] for g in geo], [g['graph'] for g in geo])
     assert [r['edges'].shape[0] for r in res] == [0, 1, 0]    # only the block with the z=5|6 face
     assert [list(r['nodes']) for r in res] == [[7], [7, 9], [9]]
+
+
+@pytest.mark.parametrize('packed', ['1', '0'])
+def test_blocks_independent_of_workspace_history(gpu, monkeypatch, packed):
+    """The same batched affinity call after a large call has grown the
+    workspace (record buffer of 2^22+ slots: the packed key+slot sort then
+    uses every one of its 64 bits) gives the result of a fresh process."""
+    monkeypatch.setenv('CTG_SORT_PACKED', packed)
+    lt, bt = rag.synth_volume((384, 384, 384), cell=10, seed=1)
+    rag.rag_features_handle(lt, bt).free()
+    del lt, bt
+    test_blocks_affinity_features(None, S.NN_OFFSETS)
+    test_blocks_affinity_features(None, S.LR_OFFSETS)
