@@ -132,10 +132,11 @@ def test_blocks_empty_and_uniform_blocks(gpu):
 @pytest.mark.parametrize('packed', ['1', '0'])
 def test_blocks_independent_of_workspace_history(gpu, monkeypatch, packed):
     """The same batched affinity call after a large call has grown the
-    workspace (record buffer of 2^22+ slots: the packed key+slot sort then
-    uses every one of its 64 bits) gives the result of a fresh process."""
+    workspace (record buffer of 2^22+ slots: 23 slot bits, which with the 32
+    tagged u bits and 9 v bits would fill the packed sort key to bit 63)
+    gives the result of a fresh process."""
     monkeypatch.setenv('CTG_SORT_PACKED', packed)
-    lt, bt = rag.synth_volume((384, 384, 384), cell=10, seed=1)
+    lt, bt = rag.synth_volume((512, 512, 512), cell=10, seed=1)
     rag.rag_features_handle(lt, bt).free()
     del lt, bt
     test_blocks_affinity_features(None, S.NN_OFFSETS)
