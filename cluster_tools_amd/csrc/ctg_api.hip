@@ -18,6 +18,8 @@
 namespace ctg {
 hipError_t launch_face_scan(const ScanParams& P, const RecordBuf& R, Counters* C, hipStream_t s);
 int scan_tile_rows();
+hipError_t launch_density(const void* L, int label_bits, const int64_t* shape, int n_rows, uint32_t* out,
+                          hipStream_t s);
 hipError_t launch_unique_tiles(const uint64_t* L, const int64_t* shape, const int64_t* b, const int64_t* e,
                                uint64_t* out, unsigned long long* count, int64_t cap, hipStream_t s);
 hipError_t launch_pack_keys(int64_t n, const uint64_t* key, int nb, uint64_t* sk, uint32_t* idx, hipStream_t s);
@@ -761,6 +763,22 @@ int ctg_rag_features(const void* labels, int label_bits, const void* data, int d
     {
         const char* xr = getenv("CTG_XCD_REMAP");
         P.xcd_remap = xr ? atoi(xr) : 1;
+    }
+    // boundary maps of fragmented volumes (configs[4]: cell 5) scan with
+    // 2-row waves: the sampled x-face density decides (cell 10 ~ 0.10,
+    // cell 5 ~ 0.20).  CTG_NARROW_ROWS=0/1 forces it.
+    if (data && n_channels == 0 && V >= (1ll << 24)) {
+        const char* nr = getenv("CTG_NARROW_ROWS");
+        if (nr) {
+            P.narrow_rows = atoi(nr);
+        } else {
+            CTG_CHECK(hipMemsetAsync(w.small + 4, 0, 8, s));
+            CTG_CHECK(launch_density(dl, label_bits, shape, 512, w.small + 4, s));
+            CTG_CHECK(hipMemcpyAsync(w.small_host + 4, w.small + 4, 8, hipMemcpyDeviceToHost, s));
+            CTG_CHECK(hipStreamSynchronize(s));
+            const double f = w.small_host[5] ? (double)w.small_host[4] / w.small_host[5] : 0.0;
+            P.narrow_rows = f > 0.14 ? 1 : 0;
+        }
     }
 
     // Long-range affinity channels: a sample counts only if its

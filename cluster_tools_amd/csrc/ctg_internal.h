@@ -126,6 +126,7 @@ struct ScanParams {
     // key is a RAG edge and the scan pushes no adjacency markers
     int skip_adj_marks;
     uint32_t lr_mask;          // bit c: channel c is long-range (|offset|_1 > 1)
+    int narrow_rows;           // boundary maps: 2-row waves (fragmented volumes, see ctg_scan.hip)
     // batched blocks (ctg_rag_blocks): workgroup w scans a tile of array b with
     // tile_prefix[b] <= w < tile_prefix[b+1]; keys carry b in the bits of u
     // from tag_shift up, so labels must stay below 2^tag_shift (else the label

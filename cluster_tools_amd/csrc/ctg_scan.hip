@@ -43,9 +43,13 @@ namespace ctg {
 
 enum { MODE_GRAPH = 0, MODE_BOUNDARY = 1, MODE_AFFINITY = 2 };
 
-constexpr int ROWS = CTG_ROWS;                            // y rows per wave, held in registers
+// y rows per wave, held in registers: 4, or 2 for highly fragmented volumes
+// (the workgroup's tile cross-section, hence its live edge set, halves: the
+// table then holds it and flushes -- records -- drop by ~40 % at cell 5)
+constexpr int ROWS_WIDE = CTG_ROWS;
+constexpr int ROWS_NARROW = 2;
 constexpr int WAVES = SCAN_THREADS / WAVE;                // 8
-constexpr int WG_ROWS = ROWS * WAVES;                     // tile y extent
+constexpr int WG_ROWS = ROWS_WIDE * WAVES;                // tile y extent (the default kernel)
 #ifndef CTG_NPER
 #define CTG_NPER 2
 #endif
@@ -485,7 +489,7 @@ __device__ __forceinline__ uint32_t shl1(uint32_t v, uint32_t edge) {
 #define FLUSH_TABLE table_flush
 #endif
 
-template <typename LabelT, typename DataT, int MODE, bool FAST40, bool BATCH>
+template <typename LabelT, typename DataT, int MODE, bool FAST40, bool BATCH, int ROWS>
 __global__ __launch_bounds__(SCAN_THREADS, 4) void k_face_scan(ScanParams P, RecordBuf R, Counters* C) {
     constexpr bool BND = MODE == MODE_BOUNDARY;
     constexpr bool AFF = MODE == MODE_AFFINITY;
@@ -566,7 +570,7 @@ __global__ __launch_bounds__(SCAN_THREADS, 4) void k_face_scan(ScanParams P, Rec
     const int tz = (int)(t / (ntx * nty));
     const int x0 = tx * TILE_X;
     const int x = x0 + lane;
-    const int yw = ty * WG_ROWS + wave * ROWS;   // first row of this wave (uniform)
+    const int yw = ty * (ROWS * WAVES) + wave * ROWS;   // first row of this wave (uniform)
     const int z0 = tz * P.tile_z;
     const int z1 = min(z0 + P.tile_z, Z);
     const LabelT* L = (const LabelT*)P.labels + l_off;
@@ -859,13 +863,13 @@ __global__ __launch_bounds__(SCAN_THREADS, 4) void k_face_scan(ScanParams P, Rec
 // ---------------------------------------------------------------------------
 // launcher
 // ---------------------------------------------------------------------------
-template <typename LabelT, typename DataT, int MODE>
-static hipError_t launch_scan_t(const ScanParams& P, const RecordBuf& R, Counters* C, hipStream_t s) {
+template <typename LabelT, typename DataT, int MODE, int NR>
+static hipError_t launch_scan_r(const ScanParams& P, const RecordBuf& R, Counters* C, hipStream_t s) {
     ScanParams Q = P;
     int64_t nwg = P.batch_tiles;
     if (!P.blocks) {
         Q.ntiles[0] = (P.shape[2] + TILE_X - 1) / TILE_X;
-        Q.ntiles[1] = (P.shape[1] + WG_ROWS - 1) / WG_ROWS;
+        Q.ntiles[1] = (P.shape[1] + NR * WAVES - 1) / (NR * WAVES);
         Q.ntiles[2] = (P.shape[0] + P.tile_z - 1) / P.tile_z;
         nwg = Q.ntiles[0] * Q.ntiles[1] * Q.ntiles[2];
     }
@@ -874,16 +878,28 @@ static hipError_t launch_scan_t(const ScanParams& P, const RecordBuf& R, Counter
     dim3 grid((unsigned)nwg);
     if (P.blocks) {
         if (P.fast40)
-            hipLaunchKernelGGL((k_face_scan<LabelT, DataT, MODE, true, true>), grid, dim3(SCAN_THREADS), 0, s, Q, R, C);
-        else
-            hipLaunchKernelGGL((k_face_scan<LabelT, DataT, MODE, false, true>), grid, dim3(SCAN_THREADS), 0, s, Q, R,
+            hipLaunchKernelGGL((k_face_scan<LabelT, DataT, MODE, true, true, NR>), grid, dim3(SCAN_THREADS), 0, s, Q, R,
                                C);
+        else
+            hipLaunchKernelGGL((k_face_scan<LabelT, DataT, MODE, false, true, NR>), grid, dim3(SCAN_THREADS), 0, s, Q,
+                               R, C);
     } else if (P.fast40) {
-        hipLaunchKernelGGL((k_face_scan<LabelT, DataT, MODE, true, false>), grid, dim3(SCAN_THREADS), 0, s, Q, R, C);
+        hipLaunchKernelGGL((k_face_scan<LabelT, DataT, MODE, true, false, NR>), grid, dim3(SCAN_THREADS), 0, s, Q, R,
+                           C);
     } else {
-        hipLaunchKernelGGL((k_face_scan<LabelT, DataT, MODE, false, false>), grid, dim3(SCAN_THREADS), 0, s, Q, R, C);
+        hipLaunchKernelGGL((k_face_scan<LabelT, DataT, MODE, false, false, NR>), grid, dim3(SCAN_THREADS), 0, s, Q, R,
+                           C);
     }
     return hipGetLastError();
+}
+
+// the narrow-tile kernel exists for whole-array boundary maps (the
+// fragmentation-bound configs[4] path); every other mode uses the wide one
+template <typename LabelT, typename DataT, int MODE>
+static hipError_t launch_scan_t(const ScanParams& P, const RecordBuf& R, Counters* C, hipStream_t s) {
+    if constexpr (MODE == MODE_BOUNDARY)
+        if (P.narrow_rows && !P.blocks) return launch_scan_r<LabelT, DataT, MODE, ROWS_NARROW>(P, R, C, s);
+    return launch_scan_r<LabelT, DataT, MODE, ROWS_WIDE>(P, R, C, s);
 }
 
 template <typename LabelT>
@@ -901,6 +917,42 @@ static hipError_t launch_scan_l(const ScanParams& P, const RecordBuf& R, Counter
 hipError_t launch_face_scan(const ScanParams& P, const RecordBuf& R, Counters* C, hipStream_t s) {
     if (P.label_bits == 32) return launch_scan_l<uint32_t>(P, R, C, s);
     return launch_scan_l<uint64_t>(P, R, C, s);
+}
+
+// Fragmentation probe: label changes along x on a sample of rows (a boundary
+// face density estimate) -- the host picks the narrow-tile scan above a
+// threshold.  One workgroup per sampled row; counts in out[0] (changes) and
+// out[1] (pairs).
+template <typename LabelT>
+__global__ __launch_bounds__(256) void k_density(const LabelT* __restrict__ L, int64_t Z, int64_t Y, int64_t X,
+                                                 uint32_t* __restrict__ out) {
+    const int64_t i = blockIdx.x;
+    const int64_t z = (i * 7919) % Z, y = (i * 104729 + 17) % Y;
+    const LabelT* row = L + (z * Y + y) * X;
+    uint32_t ch = 0, pairs = 0;
+    for (int64_t x = threadIdx.x; x + 1 < X; x += 256) {
+        ch += row[x] != row[x + 1];
+        ++pairs;
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        ch += __shfl_xor(ch, o, 64);
+        pairs += __shfl_xor(pairs, o, 64);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        atomicAdd(&out[0], ch);
+        atomicAdd(&out[1], pairs);
+    }
+}
+
+hipError_t launch_density(const void* L, int label_bits, const int64_t* shape, int n_rows, uint32_t* out,
+                          hipStream_t s) {
+    if (label_bits == 32)
+        hipLaunchKernelGGL(k_density<uint32_t>, dim3(n_rows), dim3(256), 0, s, (const uint32_t*)L, shape[0], shape[1],
+                           shape[2], out);
+    else
+        hipLaunchKernelGGL(k_density<uint64_t>, dim3(n_rows), dim3(256), 0, s, (const uint64_t*)L, shape[0], shape[1],
+                           shape[2], out);
+    return hipGetLastError();
 }
 
 int scan_tile_rows() { return WG_ROWS; }
