@@ -765,19 +765,18 @@ int ctg_rag_features(const void* labels, int label_bits, const void* data, int d
         P.xcd_remap = xr ? atoi(xr) : 1;
     }
     // boundary maps of fragmented volumes (configs[4]: cell 5) scan with
-    // 2-row waves: the sampled x-face density decides (cell 10 ~ 0.10,
-    // cell 5 ~ 0.20).  CTG_NARROW_ROWS=0/1 forces it.
+    // 2-row waves: the sampled x-face density decides on the device (cell 10
+    // ~ 0.10, cell 5 ~ 0.20 changes per pair; threshold 0.14), without a host
+    // round trip.  CTG_NARROW_ROWS=0/1 forces a width.
     if (data && n_channels == 0 && V >= (1ll << 24)) {
         const char* nr = getenv("CTG_NARROW_ROWS");
         if (nr) {
-            P.narrow_rows = atoi(nr);
+            P.narrow_rows = atoi(nr) ? 1 : 0;
         } else {
             CTG_CHECK(hipMemsetAsync(w.small + 4, 0, 8, s));
             CTG_CHECK(launch_density(dl, label_bits, shape, 512, w.small + 4, s));
-            CTG_CHECK(hipMemcpyAsync(w.small_host + 4, w.small + 4, 8, hipMemcpyDeviceToHost, s));
-            CTG_CHECK(hipStreamSynchronize(s));
-            const double f = w.small_host[5] ? (double)w.small_host[4] / w.small_host[5] : 0.0;
-            P.narrow_rows = f > 0.14 ? 1 : 0;
+            P.narrow_rows = 2;
+            P.density = w.small + 4;
         }
     }
 

@@ -126,7 +126,9 @@ struct ScanParams {
     // key is a RAG edge and the scan pushes no adjacency markers
     int skip_adj_marks;
     uint32_t lr_mask;          // bit c: channel c is long-range (|offset|_1 > 1)
-    int narrow_rows;           // boundary maps: 2-row waves (fragmented volumes, see ctg_scan.hip)
+    int narrow_rows;           // boundary maps: 1 2-row waves (fragmented volumes, see ctg_scan.hip),
+                               // 2 decided on the device from density[] (no host round trip)
+    const uint32_t* density;   // sampled x-face changes / pairs (k_density), for narrow_rows == 2
     // batched blocks (ctg_rag_blocks): workgroup w scans a tile of array b with
     // tile_prefix[b] <= w < tile_prefix[b+1]; keys carry b in the bits of u
     // from tag_shift up, so labels must stay below 2^tag_shift (else the label

@@ -497,6 +497,14 @@ __global__ __launch_bounds__(SCAN_THREADS, 4) void k_face_scan(ScanParams P, Rec
     using StageT = typename std::conditional<STATS, uint4, uint2>::type;
     __shared__ Table T;
     __shared__ StageT stage_all[WAVES][STAGE_CAP];
+    if constexpr (!BATCH) {
+        // narrow_rows == 2: both tile widths are launched back to back and the
+        // sampled face density picks the one that works (the other exits here)
+        if (P.narrow_rows == 2) {
+            const bool narrow = (uint64_t)P.density[0] * 100u > (uint64_t)P.density[1] * 14u;
+            if (narrow != (ROWS == ROWS_NARROW)) return;
+        }
+    }
     const int tid = threadIdx.x;
     const int lane = tid & (WAVE - 1);
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -897,8 +905,13 @@ static hipError_t launch_scan_r(const ScanParams& P, const RecordBuf& R, Counter
 // fragmentation-bound configs[4] path); every other mode uses the wide one
 template <typename LabelT, typename DataT, int MODE>
 static hipError_t launch_scan_t(const ScanParams& P, const RecordBuf& R, Counters* C, hipStream_t s) {
-    if constexpr (MODE == MODE_BOUNDARY)
-        if (P.narrow_rows && !P.blocks) return launch_scan_r<LabelT, DataT, MODE, ROWS_NARROW>(P, R, C, s);
+    if constexpr (MODE == MODE_BOUNDARY) {
+        if (P.narrow_rows == 2 && !P.blocks) {
+            const hipError_t e = launch_scan_r<LabelT, DataT, MODE, ROWS_WIDE>(P, R, C, s);
+            return e != hipSuccess ? e : launch_scan_r<LabelT, DataT, MODE, ROWS_NARROW>(P, R, C, s);
+        }
+        if (P.narrow_rows == 1 && !P.blocks) return launch_scan_r<LabelT, DataT, MODE, ROWS_NARROW>(P, R, C, s);
+    }
     return launch_scan_r<LabelT, DataT, MODE, ROWS_WIDE>(P, R, C, s);
 }
 

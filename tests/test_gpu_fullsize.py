@@ -30,6 +30,18 @@ RTOL = 1e-5
 N_QSAMPLE = 20000
 
 
+@pytest.fixture(autouse=True)
+def _release_device_memory():
+    """Full-size cases hold 100+ GB: hand torch's cache and the library's
+    pool back to HIP after each, so the next one starts from an empty card."""
+    yield
+    import gc
+    gc.collect()
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    rag.trim_cache()
+
+
 def _faces(lab, data, axis):
     """(keys, sample_a, sample_b) of the boundary faces along one axis."""
     sl_lo = [slice(None)] * 3
