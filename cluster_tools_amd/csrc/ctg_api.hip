@@ -767,8 +767,10 @@ int ctg_rag_features(const void* labels, int label_bits, const void* data, int d
     // boundary maps of fragmented volumes (configs[4]: cell 5) scan with
     // 2-row waves: the sampled x-face density decides on the device (cell 10
     // ~ 0.10, cell 5 ~ 0.20 changes per pair; threshold 0.14), without a host
-    // round trip.  CTG_NARROW_ROWS=0/1 forces a width.
-    if (data && n_channels == 0 && V >= (1ll << 24)) {
+    // round trip.  The probe and the second launch cost ~0.1 ms, so volumes
+    // below 2^28 voxels (~645^3, steps of ~2 ms) keep the wide tiles.
+    // CTG_NARROW_ROWS=0/1 forces a width.
+    if (data && n_channels == 0 && (V >= (1ll << 28) || getenv("CTG_NARROW_ROWS"))) {
         const char* nr = getenv("CTG_NARROW_ROWS");
         if (nr) {
             P.narrow_rows = atoi(nr) ? 1 : 0;
