@@ -48,6 +48,8 @@ hipError_t launch_bits_to_nodes(int64_t W, const uint32_t* bits, const uint32_t*
                                 hipStream_t s);
 hipError_t launch_build_adj_set(const uint64_t* edges, int64_t E, unsigned long long* set, uint32_t mask,
                                 hipStream_t s);
+hipError_t launch_build_bloom(const uint64_t* edges, int64_t E, unsigned long long* words, uint32_t mask,
+                              hipStream_t s);
 hipError_t launch_find_edges(const uint64_t* ge, int64_t n, const uint64_t* q, int64_t m, int64_t* out,
                              hipStream_t s);
 hipError_t launch_synth(uint64_t* labels, float* boundary, const int64_t* shape, int64_t z_offset,
@@ -803,7 +805,31 @@ int ctg_rag_features(const void* labels, int label_bits, const void* data, int d
             CTG_CHECK(hipMemcpyAsync(&mx, adj_graph->nodes + adj_graph->n_nodes - 1, 8, hipMemcpyDeviceToHost, s));
             CTG_CHECK(hipStreamSynchronize(s));
         }
-        if ((mx >> 32) == 0) {
+        const char* lf = getenv("CTG_LR_FILTER");
+        if ((mx >> 32) == 0 && !(lf && !strcmp(lf, "exact"))) {
+            // Bloom prefilter, 16 bits per edge: one load per long-range sample
+            // (vs. a probe chain in a set 4x the size); the reduce drops its
+            // false positives (keys no nearest-neighbour sample flagged)
+            const char* bpk = getenv("CTG_BLOOM_BPK");   // A/B: bits per edge
+            const int64_t bits = adj_graph->n_edges * (bpk ? std::max(1, atoi(bpk)) : 16);
+            uint32_t words = 1024;
+            while ((int64_t)words * 64 < bits) words *= 2;
+            adj_set = (unsigned long long*)dalloc((size_t)words * 8);
+            if (!adj_set) {
+                ctg_free(adj_graph);
+                set_error("ctg_rag_features: out of memory (adjacency filter)");
+                return CTG_ERR_NOMEM;
+            }
+            hipError_t e = launch_build_bloom(adj_graph->edges, adj_graph->n_edges, adj_set, words - 1, s);
+            if (e != hipSuccess) {
+                dfree(adj_set);
+                ctg_free(adj_graph);
+                set_error(std::string("ctg_rag_features: ") + hipGetErrorString(e));
+                return CTG_ERR_HIP;
+            }
+            P.bloom = adj_set;
+            P.bloom_mask = words - 1;
+        } else if ((mx >> 32) == 0) {
             uint32_t cap = 1024;
             while ((int64_t)cap < 2 * adj_graph->n_edges) cap *= 2;
             adj_set = (unsigned long long*)dalloc((size_t)cap * 8);
@@ -834,7 +860,7 @@ int ctg_rag_features(const void* labels, int label_bits, const void* data, int d
         // every nearest-neighbour face yields a sample of its channel, and the
         // long-range samples are filtered in the scan: all keys are RAG edges
         P.skip_adj_marks = P.n_channels > 0 && nn[0] && nn[1] && nn[2] && !(flags & CTG_NO_ADJ_FILTER) &&
-                           (!long_range || P.adj_set != nullptr);
+                           (!long_range || P.adj_set != nullptr || P.bloom != nullptr);
         if (const char* sa = getenv("CTG_SKIP_ADJ")) P.skip_adj_marks = P.skip_adj_marks && atoi(sa);
     }
     struct AdjRelease {   // the set and its graph live until the scan is done
@@ -887,6 +913,7 @@ int ctg_rag_features(const void* labels, int label_bits, const void* data, int d
     J.wide = 0;
     J.stats = stats;
     J.need_adj = P.n_channels > 0 && !P.skip_adj_marks ? ((flags & CTG_NO_ADJ_FILTER) ? 2 : 1) : 0;
+    if (P.bloom) J.need_adj = 1;   // drop the Bloom filter's false positives
     J.ignore_label = ignore_label;
     J.keep_stats = (flags & CTG_KEEP_STATS) ? 1 : 0;
     J.max_v = w.counters_host->max_v;

@@ -67,6 +67,20 @@ __host__ __device__ inline uint32_t hash_key(uint64_t k) {
     return (uint32_t)k;
 }
 
+// Blocked Bloom filter of RAG edge keys (the long-range affinity prefilter):
+// a key sets / tests 4 bits of ONE 64-bit word, so a query is a single load.
+__host__ __device__ inline uint64_t bloom_hash(uint64_t k) {
+    k ^= k >> 33;
+    k *= 0xff51afd7ed558ccdull;
+    k ^= k >> 29;
+    k *= 0xc4ceb9fe1a85ec53ull;
+    return k ^ (k >> 32);
+}
+__host__ __device__ inline uint64_t bloom_bits(uint64_t h) {
+    return (1ull << (h & 63)) | (1ull << ((h >> 6) & 63)) | (1ull << ((h >> 12) & 63)) | (1ull << ((h >> 18) & 63));
+}
+__host__ __device__ inline uint32_t bloom_word(uint64_t h, uint32_t mask) { return (uint32_t)(h >> 40) & mask; }
+
 // ---------------------------------------------------------------------------
 // records: the face scan flushes one record per (tile, edge)
 // ---------------------------------------------------------------------------
@@ -119,6 +133,11 @@ struct ScanParams {
     // addressing set of RAG edge keys ((u << 32) | v) are dropped in the scan
     const unsigned long long* adj_set;
     uint32_t adj_mask;         // set capacity - 1 (power of two)
+    // ... or a blocked Bloom filter of them (bloom_mask = words - 1): false
+    // positives are dropped by the reduce, which keeps only keys that the
+    // nearest-neighbour samples (MARK_ONE_ADJ) flagged as RAG edges
+    const unsigned long long* bloom;
+    uint32_t bloom_mask;
     int64_t ntiles[3];         // tiles along x, y, z (set by the launcher)
     int xcd_remap;             // 1: XCD-contiguous tile order (see k_face_scan)
     // affinities: the three nearest-neighbour channels are present and every

@@ -503,6 +503,21 @@ hipError_t launch_build_adj_set(const uint64_t* edges, int64_t E, unsigned long 
     return hipGetLastError();
 }
 
+__global__ void k_build_bloom(const uint64_t* __restrict__ edges, int64_t E, unsigned long long* words, uint32_t mask) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= E) return;
+    const uint64_t h = bloom_hash((edges[2 * i] << 32) | edges[2 * i + 1]);
+    atomicOr(&words[bloom_word(h, mask)], (unsigned long long)bloom_bits(h));
+}
+
+hipError_t launch_build_bloom(const uint64_t* edges, int64_t E, unsigned long long* words, uint32_t mask,
+                              hipStream_t s) {
+    hipError_t e = hipMemsetAsync(words, 0, ((size_t)mask + 1) * 8, s);
+    if (e != hipSuccess || E == 0) return e;
+    hipLaunchKernelGGL(k_build_bloom, dim3((unsigned)((E + 255) / 256)), dim3(256), 0, s, edges, E, words, mask);
+    return hipGetLastError();
+}
+
 // lexicographic binary search of (u,v) queries in a sorted (u,v) table
 __global__ void k_find_edges(const uint64_t* __restrict__ ge, int64_t n, const uint64_t* __restrict__ q,
                              int64_t m, int64_t* __restrict__ out) {

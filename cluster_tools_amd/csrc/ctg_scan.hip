@@ -76,6 +76,7 @@ constexpr uint32_t FILL_SOFT = CTG_FILL_SOFT;
 constexpr int CG = CTG_CG;
 constexpr uint32_t MARK_ADJ = 0xFFFFFFFFu;                // stage entry: nearest-neighbour face, no sample
 constexpr uint32_t MARK_ONE = 0xFFFFFFFEu;                // stage entry: one affinity sample in .z
+constexpr uint32_t MARK_ONE_ADJ = 0xFFFFFFFDu;            // ... of a nearest-neighbour face (Bloom-filtered calls)
 
 struct __align__(16) Table {
     uint64_t key[TABLE_CAP];
@@ -369,6 +370,7 @@ __device__ __forceinline__ void fold_stats(Table& T, const StageT& e, int s, Rec
         // (batched blocks) a boundary face of the block's sub-graph that the
         // block does not own -- the key is inserted, no sample counted
         const bool adj = e.w == MARK_ADJ && (AFF || e.z == MARK_ADJ);
+        const uint32_t nnf = (AFF && e.w == MARK_ONE_ADJ) ? ADJ_FLAG : 0u;   // sample that proves adjacency
         const float a = __uint_as_float(e.z);
         const float b = BND ? __uint_as_float(e.w) : a;
         const uint32_t n = adj ? 0u : (BND ? 2u : 1u);
@@ -379,7 +381,7 @@ __device__ __forceinline__ void fold_stats(Table& T, const StageT& e, int s, Rec
         const double dq = BND ? da * da + db * db : da * da;
         const uint32_t mn = f2ord(fminf(a, b)), mx = f2ord(fmaxf(a, b));
         if (s < 0) {
-            emit_direct(R, C, key, n | (adj ? ADJ_FLAG : 0u), sa, sb, adj ? 0.0 : ds, adj ? 0.0 : dq,
+            emit_direct(R, C, key, n | (adj ? ADJ_FLAG : nnf), sa, sb, adj ? 0.0 : ds, adj ? 0.0 : dq,
                         adj ? ORD_POS_INF : mn, adj ? ORD_NEG_INF : mx, true);
             return;
         }
@@ -398,6 +400,7 @@ __device__ __forceinline__ void fold_stats(Table& T, const StageT& e, int s, Rec
         atomicMin(&T.w[s][22], mn);
         atomicMax(&T.w[s][23], mx);
         atomicAdd(&T.w[s][21], n);
+        if (nnf) atomicOr(&T.w[s][21], ADJ_FLAG);
         if (ablate & 128) return;   // diagnostic: no histogram
         if constexpr (BND) hist_add2(T, s, sa, sb);
         else atomicAdd(&T.w[s][sa >> 1], 1u << ((sa & 1) * 16));
@@ -787,7 +790,20 @@ __global__ __launch_bounds__(SCAN_THREADS, 4) void k_face_scan(ScanParams P, Rec
 #pragma unroll
                             for (int j = 0; j < CG; ++j) act[j] = act[j] && lq[j] != lc;
                             // long-range channels: only pairs that are RAG edges
-                            if (P.adj_set != nullptr && ((P.lr_mask >> c0) & ((1u << CG) - 1u)) && !(ablate & 512)) {
+                            if (P.bloom != nullptr && ((P.lr_mask >> c0) & ((1u << CG) - 1u)) && !(ablate & 512)) {
+                                uint64_t hb[CG];
+                                unsigned long long wb[CG];
+                                bool lr[CG];
+#pragma unroll
+                                for (int j = 0; j < CG; ++j) {
+                                    lr[j] = act[j] && ((P.lr_mask >> (c0 + j)) & 1u);
+                                    hb[j] = bloom_hash(((uint64_t)min(lc, lq[j]) << 32) | max(lc, lq[j]));
+                                    wb[j] = lr[j] ? P.bloom[bloom_word(hb[j], P.bloom_mask)] : 0ull;
+                                }
+#pragma unroll
+                                for (int j = 0; j < CG; ++j)
+                                    if (lr[j]) act[j] = (wb[j] & bloom_bits(hb[j])) == bloom_bits(hb[j]);
+                            } else if (P.adj_set != nullptr && ((P.lr_mask >> c0) & ((1u << CG) - 1u)) && !(ablate & 512)) {
                                 uint64_t key[CG];
                                 unsigned long long k0[CG];
                                 bool lr[CG];
@@ -806,7 +822,10 @@ __global__ __launch_bounds__(SCAN_THREADS, 4) void k_face_scan(ScanParams P, Rec
                             }
 #pragma unroll
                             for (int j = 0; j < CG; ++j)
-                                if (c0 + j < P.n_channels) push(act[j], lc, lq[j], __float_as_uint(av[j]), MARK_ONE);
+                                if (c0 + j < P.n_channels)
+                                    push(act[j], lc, lq[j], __float_as_uint(av[j]),
+                                         (P.bloom != nullptr && !((P.lr_mask >> (c0 + j)) & 1u)) ? MARK_ONE_ADJ
+                                                                                                 : MARK_ONE);
                         }
                     }
                 }
