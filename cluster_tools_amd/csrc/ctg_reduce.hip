@@ -354,23 +354,25 @@ __global__ __launch_bounds__(256) void k_reduce_edges(int64_t E, const uint32_t*
     }
 }
 
+// 16 threads per edge (one per 8-B feature / 16-B stats word): the copies of
+// consecutive kept rows are coalesced
 __global__ void k_compact(int64_t E, const uint32_t* __restrict__ dE, const uint32_t* __restrict__ keep,
                           const uint32_t* __restrict__ pos, ReduceOut in, ReduceOut out, uint32_t* __restrict__ kept) {
-    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t n = min(E, (int64_t)*dE);
-    if (e == n - 1) *kept = pos[e] + keep[e];   // kept edge count
-    if (n == 0 && e == 0) *kept = 0u;
-    if (e >= n || !keep[e]) return;
-    const uint32_t p = pos[e];
-    out.edges[2 * (size_t)p] = in.edges[2 * e];
-    out.edges[2 * (size_t)p + 1] = in.edges[2 * e + 1];
-    if (in.feats)
-        for (int j = 0; j < N_FEATURES; ++j) out.feats[(size_t)p * N_FEATURES + j] = in.feats[(size_t)e * N_FEATURES + j];
-    if (in.wstats) {
-        const uint4* s = (const uint4*)(in.wstats + (size_t)e * WREC_WORDS);
-        uint4* d = (uint4*)(out.wstats + (size_t)p * WREC_WORDS);
-        for (int j = 0; j < WREC_WORDS / 4; ++j) d[j] = s[j];
-        out.wsums[p] = in.wsums[e];
+    const int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i0 == 0) *kept = n ? pos[n - 1] + keep[n - 1] : 0u;   // kept edge count
+    for (int64_t i = i0; i < n * 16; i += (int64_t)gridDim.x * blockDim.x) {   // bound by the device count
+        const int64_t e = i >> 4;
+        const int j = (int)(i & 15);
+        if (!keep[e]) continue;
+        const size_t p = pos[e];
+        if (j < 2) out.edges[2 * p + j] = in.edges[2 * e + j];
+        if (in.feats && j < N_FEATURES) out.feats[p * N_FEATURES + j] = in.feats[(size_t)e * N_FEATURES + j];
+        if (in.wstats && j < WREC_WORDS / 4) {
+            reinterpret_cast<uint4*>(out.wstats)[p * (WREC_WORDS / 4) + j] =
+                reinterpret_cast<const uint4*>(in.wstats)[(size_t)e * (WREC_WORDS / 4) + j];
+            if (j == 0) out.wsums[p] = in.wsums[e];
+        }
     }
 }
 
@@ -740,7 +742,7 @@ hipError_t launch_reduce(int64_t E, const uint32_t* dE, const uint64_t* uniq, co
 hipError_t launch_compact(int64_t E, const uint32_t* dE, const uint32_t* keep, const uint32_t* pos,
                           const ReduceOut& in, const ReduceOut& out, uint32_t* dkept, hipStream_t s) {
     if (E == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_compact, dim3((unsigned)((E + 255) / 256)), dim3(256), 0, s, E, dE, keep, pos, in, out,
+    hipLaunchKernelGGL(k_compact, dim3((unsigned)std::min<int64_t>((E * 16 + 255) / 256, 16384)), dim3(256), 0, s, E, dE, keep, pos, in, out,
                        dkept);
     return hipGetLastError();
 }
