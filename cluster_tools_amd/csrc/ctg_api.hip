@@ -46,8 +46,6 @@ hipError_t launch_mark_nodes(int64_t E, const uint32_t* dE, const uint64_t* uniq
                              hipStream_t s);
 hipError_t launch_bits_to_nodes(int64_t W, const uint32_t* bits, const uint32_t* off, uint64_t* nodes, uint32_t* dN,
                                 hipStream_t s);
-hipError_t launch_build_adj_set(const uint64_t* edges, int64_t E, unsigned long long* set, uint32_t mask,
-                                hipStream_t s);
 hipError_t launch_build_bloom(const uint64_t* edges, int64_t E, unsigned long long* words, uint32_t mask,
                               hipStream_t s);
 hipError_t launch_find_edges(const uint64_t* ge, int64_t n, const uint64_t* q, int64_t m, int64_t* out,
@@ -789,7 +787,7 @@ int ctg_rag_features(const void* labels, int label_bits, const void* data, int d
     // graph-only pass) keeps the non-adjacent pairs - most long-range pairs -
     // out of the edge tables and records.  Labels >= 2^32 skip it here: the
     // dense-relabel path re-enters with 32-bit labels and filters there.
-    unsigned long long* adj_set = nullptr;
+    unsigned long long* bloom = nullptr;
     ctg_result* adj_graph = nullptr;
     bool long_range = false;
     for (int c = 0; c < P.n_channels; ++c)
@@ -805,8 +803,7 @@ int ctg_rag_features(const void* labels, int label_bits, const void* data, int d
             CTG_CHECK(hipMemcpyAsync(&mx, adj_graph->nodes + adj_graph->n_nodes - 1, 8, hipMemcpyDeviceToHost, s));
             CTG_CHECK(hipStreamSynchronize(s));
         }
-        const char* lf = getenv("CTG_LR_FILTER");
-        if ((mx >> 32) == 0 && !(lf && !strcmp(lf, "exact"))) {
+        if ((mx >> 32) == 0) {
             // Bloom prefilter, 16 bits per edge: one load per long-range sample
             // (vs. a probe chain in a set 4x the size); the reduce drops its
             // false positives (keys no nearest-neighbour sample flagged)
@@ -814,39 +811,21 @@ int ctg_rag_features(const void* labels, int label_bits, const void* data, int d
             const int64_t bits = adj_graph->n_edges * (bpk ? std::max(1, atoi(bpk)) : 16);
             uint32_t words = 1024;
             while ((int64_t)words * 64 < bits) words *= 2;
-            adj_set = (unsigned long long*)dalloc((size_t)words * 8);
-            if (!adj_set) {
+            bloom = (unsigned long long*)dalloc((size_t)words * 8);
+            if (!bloom) {
                 ctg_free(adj_graph);
                 set_error("ctg_rag_features: out of memory (adjacency filter)");
                 return CTG_ERR_NOMEM;
             }
-            hipError_t e = launch_build_bloom(adj_graph->edges, adj_graph->n_edges, adj_set, words - 1, s);
+            hipError_t e = launch_build_bloom(adj_graph->edges, adj_graph->n_edges, bloom, words - 1, s);
             if (e != hipSuccess) {
-                dfree(adj_set);
+                dfree(bloom);
                 ctg_free(adj_graph);
                 set_error(std::string("ctg_rag_features: ") + hipGetErrorString(e));
                 return CTG_ERR_HIP;
             }
-            P.bloom = adj_set;
+            P.bloom = bloom;
             P.bloom_mask = words - 1;
-        } else if ((mx >> 32) == 0) {
-            uint32_t cap = 1024;
-            while ((int64_t)cap < 2 * adj_graph->n_edges) cap *= 2;
-            adj_set = (unsigned long long*)dalloc((size_t)cap * 8);
-            if (!adj_set) {
-                ctg_free(adj_graph);
-                set_error("ctg_rag_features: out of memory (adjacency set)");
-                return CTG_ERR_NOMEM;
-            }
-            hipError_t e = launch_build_adj_set(adj_graph->edges, adj_graph->n_edges, adj_set, cap - 1, s);
-            if (e != hipSuccess) {
-                dfree(adj_set);
-                ctg_free(adj_graph);
-                set_error(std::string("ctg_rag_features: ") + hipGetErrorString(e));
-                return CTG_ERR_HIP;
-            }
-            P.adj_set = adj_set;
-            P.adj_mask = cap - 1;
         }
     }
     {
@@ -857,10 +836,10 @@ int ctg_rag_features(const void* labels, int label_bits, const void* data, int d
             for (int a = 0; a < 3; ++a)
                 nn[a] |= o[a] == -1 && o[(a + 1) % 3] == 0 && o[(a + 2) % 3] == 0;
         }
-        // every nearest-neighbour face yields a sample of its channel, and the
-        // long-range samples are filtered in the scan: all keys are RAG edges
+        // every nearest-neighbour face yields a sample of its channel (the
+        // adjacency proof), so no separate markers are pushed
         P.skip_adj_marks = P.n_channels > 0 && nn[0] && nn[1] && nn[2] && !(flags & CTG_NO_ADJ_FILTER) &&
-                           (!long_range || P.adj_set != nullptr || P.bloom != nullptr);
+                           (!long_range || P.bloom != nullptr);
         if (const char* sa = getenv("CTG_SKIP_ADJ")) P.skip_adj_marks = P.skip_adj_marks && atoi(sa);
     }
     struct AdjRelease {   // the set and its graph live until the scan is done
@@ -874,7 +853,7 @@ int ctg_rag_features(const void* labels, int label_bits, const void* data, int d
             }
             if (g) ctg_free(g);
         }
-    } adj_release{adj_set, adj_graph, s};
+    } adj_release{bloom, adj_graph, s};
 
     Ev ev{w, s};
     ev.mark(0);

@@ -129,20 +129,17 @@ struct ScanParams {
     int check_planes;          // planes between flush decisions
     int fast40;                // histogram range [0,1) x 40 bins: exact f32 binning
     int ablate;                // diagnostic: 8 loads only, 32 staging without fold
-    // long-range affinity channels: samples whose (u,v) is not in this open-
-    // addressing set of RAG edge keys ((u << 32) | v) are dropped in the scan
-    const unsigned long long* adj_set;
-    uint32_t adj_mask;         // set capacity - 1 (power of two)
-    // ... or a blocked Bloom filter of them (bloom_mask = words - 1): false
-    // positives are dropped by the reduce, which keeps only keys that the
-    // nearest-neighbour samples (MARK_ONE_ADJ) flagged as RAG edges
+    // long-range affinity channels: samples whose (u,v) fails this blocked
+    // Bloom filter of the RAG edge keys ((u << 32) | v) are dropped in the scan
+    // (bloom_mask = words - 1); the reduce drops the false positives, keeping
+    // only keys that nearest-neighbour samples (MARK_ONE_ADJ) flagged
     const unsigned long long* bloom;
     uint32_t bloom_mask;
     int64_t ntiles[3];         // tiles along x, y, z (set by the launcher)
     int xcd_remap;             // 1: XCD-contiguous tile order (see k_face_scan)
-    // affinities: the three nearest-neighbour channels are present and every
-    // long-range sample is filtered against the RAG edge set, so every table
-    // key is a RAG edge and the scan pushes no adjacency markers
+    // affinities: the three nearest-neighbour channels are present, so every
+    // RAG edge gets a sample of one of them and the scan pushes no adjacency
+    // markers (with a Bloom filter those samples carry the flag instead)
     int skip_adj_marks;
     uint32_t lr_mask;          // bit c: channel c is long-range (|offset|_1 > 1)
     int narrow_rows;           // boundary maps: 1 2-row waves (fragmented volumes, see ctg_scan.hip),

@@ -484,27 +484,8 @@ __global__ void k_u32_to_u64(int64_t n, const uint32_t* __restrict__ in, uint64_
     if (i < n) out[i] = in[i];
 }
 
-// open-addressing set of RAG edge keys (u << 32) | v (labels < 2^32), the
-// long-range affinity filter of the face scan
-__global__ void k_build_adj_set(const uint64_t* __restrict__ edges, int64_t E, unsigned long long* set, uint32_t mask) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= E) return;
-    const uint64_t key = (edges[2 * i] << 32) | edges[2 * i + 1];
-    uint32_t h = hash_key(key) & mask;
-    for (uint32_t p = 0; p <= mask; ++p, h = (h + 1) & mask) {
-        const unsigned long long old = atomicCAS(&set[h], (unsigned long long)EMPTY_KEY, (unsigned long long)key);
-        if (old == EMPTY_KEY || old == key) return;
-    }
-}
-
-hipError_t launch_build_adj_set(const uint64_t* edges, int64_t E, unsigned long long* set, uint32_t mask,
-                                hipStream_t s) {
-    hipError_t e = hipMemsetAsync(set, 0xFF, ((size_t)mask + 1) * 8, s);
-    if (e != hipSuccess || E == 0) return e;
-    hipLaunchKernelGGL(k_build_adj_set, dim3((unsigned)((E + 255) / 256)), dim3(256), 0, s, edges, E, set, mask);
-    return hipGetLastError();
-}
-
+// blocked Bloom filter of the RAG edge keys (u << 32) | v (labels < 2^32), the
+// long-range affinity prefilter of the face scan
 __global__ void k_build_bloom(const uint64_t* __restrict__ edges, int64_t E, unsigned long long* words, uint32_t mask) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= E) return;

@@ -67,13 +67,6 @@ constexpr uint32_t FILL_SOFT = CTG_FILL_SOFT;
 #ifndef CTG_POLL_AFTER_FOLD
 #define CTG_POLL_AFTER_FOLD 1
 #endif             // request a flush past this many keys
-#ifndef CTG_CG
-#define CTG_CG 1
-#endif
-// affinity channels per load group: 1 measured best (3 nearest-neighbour
-// channels 13.3 ms scan at 1024^3 vs 16.7 ms with 4; 12 channels equal - that
-// case is bound by folding ~5 samples per voxel, not by load latency)
-constexpr int CG = CTG_CG;
 constexpr uint32_t MARK_ADJ = 0xFFFFFFFFu;                // stage entry: nearest-neighbour face, no sample
 constexpr uint32_t MARK_ONE = 0xFFFFFFFEu;                // stage entry: one affinity sample in .z
 constexpr uint32_t MARK_ONE_ADJ = 0xFFFFFFFDu;            // ... of a nearest-neighbour face (Bloom-filtered calls)
@@ -287,6 +280,13 @@ __device__ __forceinline__ float load_val(const DataT* p, int64_t i) {
     }
 }
 
+// low 32 bits of label i (a 4-B gather for 64-bit labels; little-endian)
+template <typename LabelT>
+__device__ __forceinline__ uint32_t load_lo(const LabelT* L, int64_t i) {
+    if constexpr (sizeof(LabelT) == 8) return reinterpret_cast<const uint32_t*>(L)[2 * i];
+    else return (uint32_t)L[i];
+}
+
 // vigra RangeHistogramBase binning of one float sample -> slot in [0, NSLOTS).
 // FAST40: range [0,1) x 40 bins, m = 40*x evaluated exactly as p + e (f32
 // two-product): the slot equals the double-precision rule for every x >= 0
@@ -458,18 +458,6 @@ __device__ __forceinline__ void fold_batch(Table& T, const StageT* __restrict__ 
             }
         }
         if (valid) fold_stats<MODE, FAST40, StageT>(T, e[i], s, R, C, scale, offset, need, ablate);
-    }
-}
-
-// membership of an edge key in the RAG edge set (linear probing, load <= 1/2)
-__device__ __forceinline__ bool adj_contains(const unsigned long long* __restrict__ set, uint32_t mask, uint64_t key,
-                                             uint32_t h) {
-#pragma unroll 1
-    for (;;) {
-        const unsigned long long k = set[h];
-        if (k == key) return true;
-        if (k == EMPTY_KEY) return false;
-        h = (h + 1) & mask;
     }
 }
 
@@ -758,75 +746,51 @@ __global__ __launch_bounds__(SCAN_THREADS, 4) void k_face_scan(ScanParams P, Rec
                          (own || !BATCH) ? __float_as_uint(Dc[r]) : MARK_ADJ,
                          (AFF || (BATCH && !own)) ? MARK_ADJ : __float_as_uint(Dc[r + 1]));
                 }
-                // affinity samples aff[c, p] for q = p + o_c, p in the owned box
-                if constexpr (AFF) {
-                    const int y = yw + r;
-                    if (zlo && (row_x >> r & 1u)) {
-                        const int64_t i = (int64_t)z * sz + (int64_t)y * X + x;
-                        // channels in groups of CG: the group's label gathers,
-                        // sample loads and first edge-set probes are in flight
-                        // together instead of one round trip per channel
-                        for (int c0 = 0; c0 < P.n_channels; c0 += CG) {
-                            uint32_t lq[CG];
-                            float av[CG];
-                            bool act[CG];
+            }
+            // affinity samples aff[c, p] for q = p + o_c, p in the owned box:
+            // per channel, the gathers / sample loads of all ROWS rows are in
+            // flight together, then their Bloom probes (long-range channels)
+            if constexpr (AFF) {
+                if (zlo && row_x) {
+                    const int64_t iz = (int64_t)z * sz + (int64_t)yw * X + x;
+                    for (int c = 0; c < P.n_channels; ++c) {
+                        const int qz = z + P.offsets[c][0], oy = P.offsets[c][1], qx = x + P.offsets[c][2];
+                        const bool lrc = (P.lr_mask >> c) & 1u;
+                        const bool okzx = lane_yz && qz >= 0 && qz < Z && qx >= 0 && qx < X;
+                        uint32_t lq[ROWS];
+                        float av[ROWS];
+                        bool act[ROWS];
 #pragma unroll
-                            for (int j = 0; j < CG; ++j) {
-                                const int c = c0 + j;
-                                lq[j] = lc;
-                                av[j] = 0.f;
-                                act[j] = false;
-                                if (c < P.n_channels) {
-                                    const int qz = z + P.offsets[c][0];
-                                    const int qy = y + P.offsets[c][1];
-                                    const int qx = x + P.offsets[c][2];
-                                    act[j] = lane_yz && qz >= 0 && qz < Z && qy >= 0 && qy < Y && qx >= 0 && qx < X;
-                                    if (act[j]) {
-                                        lq[j] = narrow(L[(int64_t)qz * sz + (int64_t)qy * X + qx]);
-                                        av[j] = load_val<DataT>(D, (int64_t)c * Z * sz + i);
-                                    }
-                                }
+                        for (int r = 0; r < ROWS; ++r) {
+                            const int qy = yw + r + oy;
+                            act[r] = (row_x >> r & 1u) && okzx && qy >= 0 && qy < Y;
+                            lq[r] = Lc[r];
+                            av[r] = 0.f;
+                            if (act[r]) {
+                                // the low half only: every label's high half is
+                                // checked where its own tile loads it
+                                lq[r] = load_lo(L, (int64_t)qz * sz + (int64_t)qy * X + qx);
+                                av[r] = load_val<DataT>(D, (int64_t)c * Z * sz + iz + (int64_t)r * X);
                             }
-#pragma unroll
-                            for (int j = 0; j < CG; ++j) act[j] = act[j] && lq[j] != lc;
-                            // long-range channels: only pairs that are RAG edges
-                            if (P.bloom != nullptr && ((P.lr_mask >> c0) & ((1u << CG) - 1u)) && !(ablate & 512)) {
-                                uint64_t hb[CG];
-                                unsigned long long wb[CG];
-                                bool lr[CG];
-#pragma unroll
-                                for (int j = 0; j < CG; ++j) {
-                                    lr[j] = act[j] && ((P.lr_mask >> (c0 + j)) & 1u);
-                                    hb[j] = bloom_hash(((uint64_t)min(lc, lq[j]) << 32) | max(lc, lq[j]));
-                                    wb[j] = lr[j] ? P.bloom[bloom_word(hb[j], P.bloom_mask)] : 0ull;
-                                }
-#pragma unroll
-                                for (int j = 0; j < CG; ++j)
-                                    if (lr[j]) act[j] = (wb[j] & bloom_bits(hb[j])) == bloom_bits(hb[j]);
-                            } else if (P.adj_set != nullptr && ((P.lr_mask >> c0) & ((1u << CG) - 1u)) && !(ablate & 512)) {
-                                uint64_t key[CG];
-                                unsigned long long k0[CG];
-                                bool lr[CG];
-#pragma unroll
-                                for (int j = 0; j < CG; ++j) {
-                                    lr[j] = act[j] && ((P.lr_mask >> (c0 + j)) & 1u);
-                                    key[j] = ((uint64_t)min(lc, lq[j]) << 32) | max(lc, lq[j]);
-                                    k0[j] = lr[j] ? P.adj_set[hash_key(key[j]) & P.adj_mask] : EMPTY_KEY;
-                                }
-#pragma unroll
-                                for (int j = 0; j < CG; ++j)
-                                    if (lr[j] && k0[j] != key[j])
-                                        act[j] = k0[j] != EMPTY_KEY &&
-                                                 adj_contains(P.adj_set, P.adj_mask, key[j],
-                                                              (hash_key(key[j]) + 1u) & P.adj_mask);
-                            }
-#pragma unroll
-                            for (int j = 0; j < CG; ++j)
-                                if (c0 + j < P.n_channels)
-                                    push(act[j], lc, lq[j], __float_as_uint(av[j]),
-                                         (P.bloom != nullptr && !((P.lr_mask >> (c0 + j)) & 1u)) ? MARK_ONE_ADJ
-                                                                                                 : MARK_ONE);
                         }
+#pragma unroll
+                        for (int r = 0; r < ROWS; ++r) act[r] = act[r] && lq[r] != Lc[r];
+                        // long-range channels: only pairs that are RAG edges
+                        if (lrc && P.bloom != nullptr && !(ablate & 512)) {
+                            uint64_t hb[ROWS];
+                            unsigned long long wb[ROWS];
+#pragma unroll
+                            for (int r = 0; r < ROWS; ++r) {
+                                hb[r] = bloom_hash(((uint64_t)min(Lc[r], lq[r]) << 32) | max(Lc[r], lq[r]));
+                                wb[r] = act[r] ? P.bloom[bloom_word(hb[r], P.bloom_mask)] : 0ull;
+                            }
+#pragma unroll
+                            for (int r = 0; r < ROWS; ++r)
+                                act[r] = act[r] && (wb[r] & bloom_bits(hb[r])) == bloom_bits(hb[r]);
+                        }
+                        const uint32_t mk = (P.bloom != nullptr && !lrc) ? MARK_ONE_ADJ : MARK_ONE;
+#pragma unroll
+                        for (int r = 0; r < ROWS; ++r) push(act[r], Lc[r], lq[r], __float_as_uint(av[r]), mk);
                     }
                 }
             }
