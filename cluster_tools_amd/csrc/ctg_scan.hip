@@ -50,6 +50,12 @@ constexpr int ROWS_WIDE = CTG_ROWS;
 constexpr int ROWS_NARROW = 2;
 constexpr int WAVES = SCAN_THREADS / WAVE;                // 8
 constexpr int WG_ROWS = ROWS_WIDE * WAVES;                // tile y extent (the default kernel)
+#ifndef CTG_AFF_G
+#define CTG_AFF_G 2
+#endif
+// affinity channels whose gathers / sample loads / Bloom probes are issued
+// together (x ROWS rows): the channel loop is bound by memory round trips
+constexpr int AFF_G = CTG_AFF_G;
 #ifndef CTG_NPER
 #define CTG_NPER 2
 #endif
@@ -753,44 +759,59 @@ __global__ __launch_bounds__(SCAN_THREADS, 4) void k_face_scan(ScanParams P, Rec
             if constexpr (AFF) {
                 if (zlo && row_x) {
                     const int64_t iz = (int64_t)z * sz + (int64_t)yw * X + x;
-                    for (int c = 0; c < P.n_channels; ++c) {
-                        const int qz = z + P.offsets[c][0], oy = P.offsets[c][1], qx = x + P.offsets[c][2];
-                        const bool lrc = (P.lr_mask >> c) & 1u;
-                        const bool okzx = lane_yz && qz >= 0 && qz < Z && qx >= 0 && qx < X;
-                        uint32_t lq[ROWS];
-                        float av[ROWS];
-                        bool act[ROWS];
+                    for (int c0 = 0; c0 < P.n_channels; c0 += AFF_G) {
+                        constexpr int K = AFF_G * ROWS;   // (channel, row) sites of the group
+                        uint32_t lq[K];
+                        float av[K];
+                        bool act[K];
 #pragma unroll
-                        for (int r = 0; r < ROWS; ++r) {
-                            const int qy = yw + r + oy;
-                            act[r] = (row_x >> r & 1u) && okzx && qy >= 0 && qy < Y;
-                            lq[r] = Lc[r];
-                            av[r] = 0.f;
-                            if (act[r]) {
-                                // the low half only: every label's high half is
-                                // checked where its own tile loads it
-                                lq[r] = load_lo(L, (int64_t)qz * sz + (int64_t)qy * X + qx);
-                                av[r] = load_val<DataT>(D, (int64_t)c * Z * sz + iz + (int64_t)r * X);
-                            }
-                        }
-#pragma unroll
-                        for (int r = 0; r < ROWS; ++r) act[r] = act[r] && lq[r] != Lc[r];
-                        // long-range channels: only pairs that are RAG edges
-                        if (lrc && P.bloom != nullptr && !(ablate & 512)) {
-                            uint64_t hb[ROWS];
-                            unsigned long long wb[ROWS];
+                        for (int j = 0; j < AFF_G; ++j) {
+                            const int c = c0 + j;
+                            const bool has = c < P.n_channels;
+                            const int qz = has ? z + P.offsets[c][0] : -1, oy = has ? P.offsets[c][1] : 0;
+                            const int qx = has ? x + P.offsets[c][2] : -1;
+                            const bool okzx = lane_yz && qz >= 0 && qz < Z && qx >= 0 && qx < X;
 #pragma unroll
                             for (int r = 0; r < ROWS; ++r) {
-                                hb[r] = bloom_hash(((uint64_t)min(Lc[r], lq[r]) << 32) | max(Lc[r], lq[r]));
-                                wb[r] = act[r] ? P.bloom[bloom_word(hb[r], P.bloom_mask)] : 0ull;
+                                const int k = j * ROWS + r;
+                                const int qy = yw + r + oy;
+                                act[k] = (row_x >> r & 1u) && okzx && qy >= 0 && qy < Y;
+                                lq[k] = Lc[r];
+                                av[k] = 0.f;
+                                if (act[k]) {
+                                    // the low half only: every label's high half is
+                                    // checked where its own tile loads it
+                                    lq[k] = load_lo(L, (int64_t)qz * sz + (int64_t)qy * X + qx);
+                                    av[k] = load_val<DataT>(D, (int64_t)c * Z * sz + iz + (int64_t)r * X);
+                                }
+                            }
+                        }
+#pragma unroll
+                        for (int k = 0; k < K; ++k) act[k] = act[k] && lq[k] != Lc[k % ROWS];
+                        // long-range channels: only pairs that are RAG edges
+                        const uint32_t glr = (P.lr_mask >> c0) & ((1u << AFF_G) - 1u);
+                        if (glr && P.bloom != nullptr && !(ablate & 512)) {
+                            uint64_t hb[K];
+                            unsigned long long wb[K];
+#pragma unroll
+                            for (int k = 0; k < K; ++k) {
+                                const uint32_t lc = Lc[k % ROWS];
+                                hb[k] = bloom_hash(((uint64_t)min(lc, lq[k]) << 32) | max(lc, lq[k]));
+                                wb[k] = (act[k] && (glr >> (k / ROWS) & 1u)) ? P.bloom[bloom_word(hb[k], P.bloom_mask)]
+                                                                             : ~0ull;
                             }
 #pragma unroll
-                            for (int r = 0; r < ROWS; ++r)
-                                act[r] = act[r] && (wb[r] & bloom_bits(hb[r])) == bloom_bits(hb[r]);
+                            for (int k = 0; k < K; ++k)
+                                act[k] = act[k] && (wb[k] & bloom_bits(hb[k])) == bloom_bits(hb[k]);
                         }
-                        const uint32_t mk = (P.bloom != nullptr && !lrc) ? MARK_ONE_ADJ : MARK_ONE;
 #pragma unroll
-                        for (int r = 0; r < ROWS; ++r) push(act[r], Lc[r], lq[r], __float_as_uint(av[r]), mk);
+                        for (int j = 0; j < AFF_G; ++j) {
+                            if (c0 + j >= P.n_channels) break;
+                            const uint32_t mk = (P.bloom != nullptr && !(glr >> j & 1u)) ? MARK_ONE_ADJ : MARK_ONE;
+#pragma unroll
+                            for (int r = 0; r < ROWS; ++r)
+                                push(act[j * ROWS + r], Lc[r], lq[j * ROWS + r], __float_as_uint(av[j * ROWS + r]), mk);
+                        }
                     }
                 }
             }
