@@ -77,11 +77,14 @@ def parse():
     return p.parse_args()
 
 
-def pmc_traffic_per_launch():
-    """HBM bytes per face-scan launch from the committed rocprofv3 PMC summary
-    (profiles/*/pmc_summary.json, written by tools/pmc_summary.py), or None."""
+def pmc_traffic_per_launch(config='1'):
+    """HBM bytes per face-scan launch of BASELINE config ``config`` at its
+    default size, from the newest committed rocprofv3 PMC summary
+    (profiles/*/pmc_summary.json for config 1, pmc_summary_c<config>.json for
+    the others; written by tools/pmc_summary.py), or None."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, 'profiles', '*', 'pmc_summary.json')))
+    name = 'pmc_summary.json' if config == '1' else 'pmc_summary_c%s.json' % config
+    files = sorted(glob.glob(os.path.join(ROOT, 'profiles', '*', name)))
     for f in reversed(files):
         try:
             with open(f) as fh:
@@ -361,7 +364,9 @@ def main():
     vox_bytes = 8 + 4 * n_ch
     scan_bytes = V * vox_bytes
     achieved = scan_bytes / (scan_avg_ms * 1e-3) / 1e9
-    traffic, traffic_src = pmc_traffic_per_launch() if args.config == '1' else (None, None)
+    traffic, traffic_src = (pmc_traffic_per_launch(args.config)
+                            if not args.size and not args.cell and (scaling == 'weak' or world == 1)
+                            else (None, None))
     step_bytes = total_vox * vox_bytes + n_edges * EDGE_BYTES
 
     line = None
