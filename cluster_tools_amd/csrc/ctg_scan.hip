@@ -293,26 +293,20 @@ __device__ __forceinline__ uint32_t load_lo(const LabelT* L, int64_t i) {
     else return (uint32_t)L[i];
 }
 
-// vigra RangeHistogramBase binning of one float sample -> slot in [0, NSLOTS).
-// FAST40: range [0,1) x 40 bins, m = 40*x evaluated exactly as p + e (f32
-// two-product): the slot equals the double-precision rule for every x >= 0
-// (m == 40 -> bin 39, m > 40 -> right outlier); negative / NaN samples take
-// the double path.
+// vigra RangeHistogramBase binning of one sample -> slot in [0, NSLOTS)
+// (hist_slot's rule, ctg_internal.h), branch-free on the f64 value the sums
+// use anyway: m = scale * (x - offset); FAST40 (offset 0, scale 40) skips the
+// subtraction -- 40 * x is exact in f64 for every float x, so the slot is the
+// double-precision rule's.  Selects instead of branches: no exec-mask
+// juggling in the fold.
 template <bool FAST40>
-__device__ __forceinline__ int sample_slot(float x, double scale, double offset) {
-    if constexpr (FAST40) {
-        if (x >= 0.f) {
-            const float p = x * 40.0f;
-            const float e = __builtin_fmaf(x, 40.0f, -p);
-            float fl = __builtin_floorf(p);
-            fl = (fl == p && e < 0.0f) ? fl - 1.0f : fl;   // true m just below an integer p
-            fl = __builtin_fminf(fl, 40.0f);                  // +inf / huge -> right outlier
-            int s = (int)fl + 1;
-            s = (p == 40.0f && e == 0.0f) ? NBINS : s;        // m == 40 exactly -> last bin
-            return s > NBINS + 1 ? NBINS + 1 : s;
-        }
-    }
-    return hist_slot((double)x, scale, offset);
+__device__ __forceinline__ int sample_slot(double dx, double scale, double offset) {
+    const double m = FAST40 ? dx * 40.0 : scale * (dx - offset);
+    int s = (int)m + 1;                              // trunc toward zero (v_cvt_i32_f64 saturates)
+    s = m <= -1.0 ? 0 : s;                           // left outlier
+    s = !(m < (double)NBINS) ? NBINS + 1 : s;        // right outlier
+    s = m != m ? 0 : s;                              // NaN -> left
+    return m == (double)NBINS ? NBINS : s;           // index nbins-1
 }
 
 // 2-sample histogram add: one atomic when both samples share a word
@@ -362,7 +356,7 @@ __device__ __forceinline__ int bucket_match(const uint4& b01, const uint4& b23, 
 }
 
 // statistics of one staged entry into table slot s (s < 0: direct record)
-template <int MODE, bool FAST40, typename StageT>
+template <int MODE, bool FAST40, bool BATCH, typename StageT>
 __device__ __forceinline__ void fold_stats(Table& T, const StageT& e, int s, RecordBuf R, Counters* C, double scale,
                                            double offset, bool& need, int ablate) {
     constexpr bool BND = MODE == MODE_BOUNDARY;
@@ -375,14 +369,14 @@ __device__ __forceinline__ void fold_stats(Table& T, const StageT& e, int s, Rec
         // adjacency-only entries: a nearest-neighbour face of an affinity map, or
         // (batched blocks) a boundary face of the block's sub-graph that the
         // block does not own -- the key is inserted, no sample counted
-        const bool adj = e.w == MARK_ADJ && (AFF || e.z == MARK_ADJ);
+        const bool adj = (AFF || BATCH) && e.w == MARK_ADJ && (AFF || e.z == MARK_ADJ);
         const uint32_t nnf = (AFF && e.w == MARK_ONE_ADJ) ? ADJ_FLAG : 0u;   // sample that proves adjacency
         const float a = __uint_as_float(e.z);
         const float b = BND ? __uint_as_float(e.w) : a;
         const uint32_t n = adj ? 0u : (BND ? 2u : 1u);
-        const int sa = adj ? -1 : sample_slot<FAST40>(a, scale, offset);
-        const int sb = (BND && !adj) ? sample_slot<FAST40>(b, scale, offset) : -1;
         const double da = (double)a, db = (double)b;
+        const int sa = adj ? -1 : sample_slot<FAST40>(da, scale, offset);
+        const int sb = (BND && !adj) ? sample_slot<FAST40>(db, scale, offset) : -1;
         const double ds = BND ? da + db : da;
         const double dq = BND ? da * da + db * db : da * da;
         const uint32_t mn = f2ord(fminf(a, b)), mx = f2ord(fmaxf(a, b));
@@ -416,7 +410,7 @@ __device__ __forceinline__ void fold_stats(Table& T, const StageT& e, int s, Rec
 // Fold the wave's nb staged entries into the LDS edge table: NPER entries per
 // lane (lane, lane+64, ...), their stage reads and home-bucket reads issued
 // together so the LDS round trips of the entries overlap.
-template <int MODE, bool FAST40, typename StageT, int NPER>
+template <int MODE, bool FAST40, bool BATCH, typename StageT, int NPER>
 __device__ __forceinline__ void fold_batch(Table& T, const StageT* __restrict__ stage, int nb, int lane, RecordBuf R,
                                            Counters* C, double scale, double offset, bool& need, int ablate) {
     StageT e[NPER];
@@ -463,7 +457,7 @@ __device__ __forceinline__ void fold_batch(Table& T, const StageT* __restrict__ 
                 }
             }
         }
-        if (valid) fold_stats<MODE, FAST40, StageT>(T, e[i], s, R, C, scale, offset, need, ablate);
+        if (valid) fold_stats<MODE, FAST40, BATCH, StageT>(T, e[i], s, R, C, scale, offset, need, ablate);
     }
 }
 
@@ -581,7 +575,11 @@ __global__ __launch_bounds__(SCAN_THREADS, 4) void k_face_scan(ScanParams P, Rec
     const LabelT* L = (const LabelT*)P.labels + l_off;
     const DataT* D = (const DataT*)P.data + d_off;
     const double scale = P.scale, offset = P.offset;
-    const int ablate = P.ablate;
+#ifdef CTG_DIAG
+    const int ablate = P.ablate;   // diagnostic builds only (make variant EXTRA=-DCTG_DIAG)
+#else
+    constexpr int ablate = 0;      // product kernels carry no diagnostic branches
+#endif
     const uint32_t hi_mask = BATCH ? P.label_hi_mask : 0u;
     // lane masks (x is per lane): faces are owned by their upper voxel
     const bool inx = x < X;
@@ -685,7 +683,7 @@ __global__ __launch_bounds__(SCAN_THREADS, 4) void k_face_scan(ScanParams P, Rec
                 wsamp += add;
             }
             const uint64_t t0 = stamps ? stamp_now() : 0;
-            fold_batch<MODE, FAST40, StageT, NPER>(T, stage, nbuf, lane, R, C, scale, offset, need, ablate);
+            fold_batch<MODE, FAST40, BATCH, StageT, NPER>(T, stage, nbuf, lane, R, C, scale, offset, need, ablate);
             nbuf = 0;
             if (stamps) t_fold += stamp_now() - t0;
 #if CTG_POLL_AFTER_FOLD
@@ -695,7 +693,7 @@ __global__ __launch_bounds__(SCAN_THREADS, 4) void k_face_scan(ScanParams P, Rec
     };
     // append the active lanes of one site to the stage
     auto push = [&](bool act, uint32_t a, uint32_t b, uint32_t za, uint32_t zb) {
-        const uint64_t m = __ballot(act);
+        const uint64_t m = __builtin_amdgcn_ballot_w64(act);
         if (m == 0) return;
         const int k = __popcll(m);
         if (nbuf + k > STAGE_CAP) flush_stage();
