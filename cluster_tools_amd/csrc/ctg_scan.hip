@@ -604,7 +604,6 @@ __global__ __launch_bounds__(SCAN_THREADS, 4) void k_face_scan(ScanParams P, Rec
     // blocks always push them (the block's sub-graph is the edge filter)
     const bool adj_marks = AFF && (batch || !P.skip_adj_marks);
     const int xh = x0 + TILE_X;              // x of the lane-63 neighbour
-    const bool has_xh = xh < X;
 
     // plane buffers: rows 0..ROWS-1 of this wave + the y-halo row; the x-halo
     // voxel of row r lives in lane r of XL / XD
@@ -624,24 +623,29 @@ __global__ __launch_bounds__(SCAN_THREADS, 4) void k_face_scan(ScanParams P, Rec
         if constexpr (BATCH) ovf |= (uint32_t)l & hi_mask;   // batched blocks: the tag bits must be free
         return (uint32_t)l;
     };
+    // Loads are unconditional: rows past Y and lanes past X read the clamped
+    // row / column (valid memory; every face and sample of such a row or lane
+    // is masked by row_x / row_y / lane_xf / lane_yz), so no exec-mask
+    // branches and no default moves sit between the loads.
+    const int xcl = min(x, X - 1);
+    const int xhc = min(xh, X - 1);
     auto load_plane = [&](int z, LabelT (&Lb)[ROWS + 1], float (&Db)[ROWS + 1], LabelT& XL, float& XD) {
         const LabelT* Lz = L + (int64_t)z * sz + (int64_t)yw * X;
         const DataT* Dz = BND ? D + (int64_t)z * sz + (int64_t)yw * X : nullptr;
+        const int rmax = Y - 1 - yw;   // last valid row offset (uniform; < 0 only for waves past Y)
 #pragma unroll
         for (int r = 0; r <= ROWS; ++r) {
-            Lb[r] = 0;
-            Db[r] = 0.f;
-            if (yw + r < Y && inx) {
-                Lb[r] = Lz[r * X + x];
-                if constexpr (BND) Db[r] = load_val<DataT>(Dz, r * X + x);
-            }
+            const int rr = min(r, rmax);
+            Lb[r] = Lz[(int64_t)rr * X + xcl];
+            if constexpr (BND) Db[r] = load_val<DataT>(Dz, (int64_t)rr * X + xcl);
+            else Db[r] = 0.f;
         }
-        XL = 0;
-        XD = 0.f;
-        if (lane < ROWS && has_xh && yw + lane < Y) {
-            XL = Lz[lane * X + xh];
-            if constexpr (BND) XD = load_val<DataT>(Dz, lane * X + xh);
-        }
+        // x-halo: lane r < ROWS holds row r's voxel at x = x0 + 64 (lanes past
+        // ROWS repeat row ROWS - 1; only lanes < ROWS are read)
+        const int hr = min(min(lane, ROWS - 1), rmax);
+        XL = Lz[(int64_t)hr * X + xhc];
+        if constexpr (BND) XD = load_val<DataT>(Dz, (int64_t)hr * X + xhc);
+        else XD = 0.f;
     };
 
     // Flushes on demand: a wave whose fold found the table past FILL_SOFT (or
@@ -712,9 +716,12 @@ __global__ __launch_bounds__(SCAN_THREADS, 4) void k_face_scan(ScanParams P, Rec
         for (int r = 0; r <= ROWS; ++r) Lc[r] = narrow(Ln[r]);
         XLc = narrow(XLn);
     }
+    __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): nothing in flight when the plane loop starts
     for (int z = z0; z < z1; ++z) {
         const bool hz = z + 1 < Z;
-        if (hz) load_plane(z + 1, Ln, Dn, XLn, XDn);        // prefetch: in flight during x/y faces
+        // prefetch, unconditional (the last plane re-reads itself; its z faces
+        // are masked by hz): in flight during the x / y faces
+        load_plane(hz ? z + 1 : z, Ln, Dn, XLn, XDn);
         const bool zlo = z >= obz && z < oez;
         const bool zup = hz && z + 1 >= obz && z + 1 < oez;
         const bool zg = batch && z >= gbz && z < gez;            // graph box planes (batched)
@@ -836,6 +843,11 @@ __global__ __launch_bounds__(SCAN_THREADS, 4) void k_face_scan(ScanParams P, Rec
         // staged entries stay staged across planes (raw faces are valid for
         // whatever table they are folded into later)
         poll();
+        // the prefetched plane has landed by now (it had the whole plane's work
+        // to do so): wait for it here, before the next plane's loads are
+        // issued -- a wait placed after them (where the compiler would put it
+        // on first use) would drain the new prefetch too
+        __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
 #pragma unroll
         for (int r = 0; r <= ROWS; ++r) {
             Lc[r] = narrow(Ln[r]);
