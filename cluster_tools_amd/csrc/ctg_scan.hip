@@ -123,73 +123,6 @@ __device__ __forceinline__ void lds_barrier() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 
-template <int MODE>
-__device__ __noinline__ void table_flush(Table& T, RecordBuf R, Counters* C) {
-    static_assert(TABLE_CAP == SCAN_THREADS, "one table entry per thread in the flush");
-    lds_barrier();
-    const int tid = threadIdx.x;
-    const int lane = tid & (WAVE - 1), wv = tid >> 6;
-    // ballot compaction: entry tid goes to wave offset + rank among its wave
-    const uint64_t k = T.key[tid];
-    const bool live = k != EMPTY_KEY;
-    const uint64_t m = __ballot(live);
-    const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
-    uint32_t mv = live ? (uint32_t)k : 0u;
-    for (int o = 32; o > 0; o >>= 1) mv = max(mv, (uint32_t)__shfl_xor((int)mv, o, WAVE));
-    if (lane == 0) {
-        T.wave_cnt[wv] = (uint32_t)__popcll(m);
-        if (mv) atomicMax(&T.maxv, (unsigned long long)mv);
-    }
-    lds_barrier();
-    uint32_t off = 0, n = 0;
-#pragma unroll
-    for (int w = 0; w < WAVES; ++w) {
-        off += w < wv ? T.wave_cnt[w] : 0u;
-        n += T.wave_cnt[w];
-    }
-    if (live) T.compact[off + rank] = (uint16_t)tid;
-    if (tid == 0) T.ncompact = n;
-    lds_barrier();
-    const int reg = blockIdx.x & (NREG - 1);
-    if (tid == 0 && n) T.base = atomicAdd(&C->rcount[reg], (unsigned long long)n);
-    lds_barrier();
-    if (n) {
-        const unsigned long long base = T.base;
-        const unsigned long long rcap = (unsigned long long)R.rcap, slot0 = (unsigned long long)reg * rcap + base;
-        for (uint32_t r = tid; r < n; r += SCAN_THREADS) {
-            const int e = T.compact[r];
-            if (base + r < rcap) R.key[slot0 + r] = T.key[e];
-        }
-        if (MODE != MODE_GRAPH) {
-            // coalesced copy into the 128-byte record bodies
-            for (uint32_t f = tid; f < n * NREC_STRIDE; f += SCAN_THREADS) {
-                const uint32_t r = f / NREC_STRIDE, j = f % NREC_STRIDE;
-                const int e = T.compact[r];
-                uint32_t val = 0u;
-                if (j < NREC_OFF) {
-                    const uint32_t* sw = reinterpret_cast<const uint32_t*>(j < 2 ? &T.sum[e] : &T.sq[e]);
-                    val = sw[j & 1];
-                } else if (j < NREC_OFF + NREC_WORDS) {
-                    val = T.w[e][j - NREC_OFF];
-                }
-                if (base + r < rcap) R.hist[(slot0 + r) * NREC_STRIDE + j] = val;
-            }
-        }
-        lds_barrier();
-        for (uint32_t r = tid; r < n; r += SCAN_THREADS) entry_reset(T, T.compact[r]);
-    }
-    lds_barrier();
-    if (tid == 0) {
-        T.used = 0;
-        T.ncompact = 0;
-        T.flush_req = 0;
-    }
-    lds_barrier();
-}
-
-#ifndef CTG_WAVE_FLUSH
-#define CTG_WAVE_FLUSH 1
-#endif
 // Flush by waves: every wave writes out the live entries among its own 64
 // table slots (entry tid) - its own record range from one global atomic, its
 // own 128-byte bodies, its own resets - so the flush needs two workgroup
@@ -229,7 +162,11 @@ __device__ __noinline__ void table_flush_waves(Table& T, RecordBuf R, Counters* 
         }
         __builtin_amdgcn_wave_barrier();
         if (MODE != MODE_GRAPH) {
-            // 16-byte pieces of the 128-byte bodies: piece q of record r
+            // 16-byte pieces of the 128-byte bodies: piece q of record r (eight
+            // consecutive lanes per record; n * 8 is a multiple of 8, so a
+            // record's lanes are active together).  The sample count is not
+            // kept in the table (one atomic less per face): it is the sum of
+            // the 42 u16 histogram slots, reduced over the record's lanes here.
             for (uint32_t f = lane; f < n * 8; f += WAVE) {
                 const uint32_t r = f >> 3, q = f & 7;
                 const int e = cw[r];
@@ -241,6 +178,14 @@ __device__ __noinline__ void table_flush_waves(Table& T, RecordBuf R, Counters* 
                     const uint32_t* w = &T.w[e][4 * (q - 1)];
                     val = make_uint4(w[0], w[1], w[2], w[3]);
                 }
+                // histogram words 0..20 sit in pieces 1..5 and piece 6's .x
+                auto h2 = [](uint32_t v) { return (v & 0xFFFFu) + (v >> 16); };
+                uint32_t c = (q >= 1 && q <= 5) ? h2(val.x) + h2(val.y) + h2(val.z) + h2(val.w)
+                                                : (q == 6 ? h2(val.x) : 0u);
+                c += (uint32_t)__shfl_xor((int)c, 1, WAVE);
+                c += (uint32_t)__shfl_xor((int)c, 2, WAVE);
+                c += (uint32_t)__shfl_xor((int)c, 4, WAVE);
+                if (q == 6) val.y |= c;   // word 21: count | ADJ
                 if (base + r < rcap) reinterpret_cast<uint4*>(R.hist + (slot0 + r) * NREC_STRIDE)[q] = val;
             }
         }
@@ -399,7 +344,8 @@ __device__ __forceinline__ void fold_stats(Table& T, const StageT& e, int s, Rec
         atomicAdd(&T.sq[s], dq);
         atomicMin(&T.w[s][22], mn);
         atomicMax(&T.w[s][23], mx);
-        atomicAdd(&T.w[s][21], n);
+        // word 21 carries only the ADJ flag in the table; the count is the
+        // histogram's sum, filled in by the flush
         if (nnf) atomicOr(&T.w[s][21], ADJ_FLAG);
         if (ablate & 128) return;   // diagnostic: no histogram
         if constexpr (BND) hist_add2(T, s, sa, sb);
@@ -474,11 +420,7 @@ __device__ __forceinline__ uint32_t shl1(uint32_t v, uint32_t edge) {
     return (uint32_t)__builtin_amdgcn_update_dpp((int)edge, (int)v, 0x130, 0xf, 0xf, false);
 }
 
-#if CTG_WAVE_FLUSH
 #define FLUSH_TABLE table_flush_waves
-#else
-#define FLUSH_TABLE table_flush
-#endif
 
 template <typename LabelT, typename DataT, int MODE, bool FAST40, bool BATCH, int ROWS>
 __global__ __launch_bounds__(SCAN_THREADS, 4) void k_face_scan(ScanParams P, RecordBuf R, Counters* C) {
@@ -613,6 +555,10 @@ __global__ __launch_bounds__(SCAN_THREADS, 4) void k_face_scan(ScanParams P, Rec
     uint32_t Lc[ROWS + 1];
     LabelT Ln[ROWS + 1];
     float Dc[ROWS + 1], Dn[ROWS + 1];
+    // previous plane (rows 0..ROWS-1): z faces pair plane z-1 with plane z,
+    // so a plane's faces never wait on the plane being prefetched
+    uint32_t Lp[ROWS];
+    float Dp[ROWS];
     uint32_t XLc = 0;
     LabelT XLn = 0;
     float XDc = 0.f, XDn = 0.f;
@@ -697,8 +643,9 @@ __global__ __launch_bounds__(SCAN_THREADS, 4) void k_face_scan(ScanParams P, Rec
     };
     // append the active lanes of one site to the stage
     auto push = [&](bool act, uint32_t a, uint32_t b, uint32_t za, uint32_t zb) {
+        // no early-out on an empty ballot: at ~15 % face density a site is
+        // almost never empty, and k = 0 makes the rest a no-op
         const uint64_t m = __builtin_amdgcn_ballot_w64(act);
-        if (m == 0) return;
         const int k = __popcll(m);
         if (nbuf + k > STAGE_CAP) flush_stage();
         const int rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
@@ -710,8 +657,20 @@ __global__ __launch_bounds__(SCAN_THREADS, 4) void k_face_scan(ScanParams P, Rec
         nbuf += k;
     };
 
+    // z faces are visited at their upper voxel's plane: a tile owns the faces
+    // (z-1, z) for z in [z0, z1), so it starts from plane z0 - 1 (kept as the
+    // previous plane only)
+    const bool has_prev = z0 > 0;
     if (z0 < z1) {
+        load_plane(has_prev ? z0 - 1 : z0, Ln, Dn, XLn, XDn);
+        __builtin_amdgcn_s_waitcnt(0x0F70);
+#pragma unroll
+        for (int r = 0; r < ROWS; ++r) {
+            Lp[r] = narrow(Ln[r]);
+            Dp[r] = Dn[r];
+        }
         load_plane(z0, Ln, Dc, XLn, XDc);
+        __builtin_amdgcn_s_waitcnt(0x0F70);
 #pragma unroll
         for (int r = 0; r <= ROWS; ++r) Lc[r] = narrow(Ln[r]);
         XLc = narrow(XLn);
@@ -719,13 +678,13 @@ __global__ __launch_bounds__(SCAN_THREADS, 4) void k_face_scan(ScanParams P, Rec
     __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): nothing in flight when the plane loop starts
     for (int z = z0; z < z1; ++z) {
         const bool hz = z + 1 < Z;
-        // prefetch, unconditional (the last plane re-reads itself; its z faces
-        // are masked by hz): in flight during the x / y faces
+        // prefetch of plane z + 1, unconditional (the last plane re-reads
+        // itself): in flight during all of plane z's faces
         load_plane(hz ? z + 1 : z, Ln, Dn, XLn, XDn);
         const bool zlo = z >= obz && z < oez;
-        const bool zup = hz && z + 1 >= obz && z + 1 < oez;
+        const bool zup = z > 0 && zlo;                          // face (z-1, z): upper voxel in the own box
         const bool zg = batch && z >= gbz && z < gez;            // graph box planes (batched)
-        const bool gzup = zg && z + 1 < gez;
+        const bool gzup = zg && z - 1 >= gbz;
         if (ablate & 8) {   // diagnostic: loads only
             uint32_t chk = 0;
 #pragma unroll
@@ -820,22 +779,16 @@ __global__ __launch_bounds__(SCAN_THREADS, 4) void k_face_scan(ScanParams P, Rec
                     }
                 }
             }
-            // z faces: plane z against the prefetched plane z+1
-            if (stamps) {
-                const uint64_t t0 = stamp_now();
-                __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): the prefetched plane has landed
-                t_wait += stamp_now() - t0;
-            }
+            // z faces (z-1, z): the previous plane against plane z
             if ((zup || gzup) && (!AFF || adj_marks)) {
 #pragma unroll
                 for (int r = 0; r < ROWS; ++r) {
-                    const uint32_t ln = (uint32_t)Ln[r];
                     const bool zo = zup && (row_x >> r & 1u), zgr = gzup && (grow_x >> r & 1u);
                     if (zo || zgr) {
                         const bool own = zo && lane_yz;
-                        push((own || (zgr && glane_yz)) && Lc[r] != ln, Lc[r], ln,
-                             (own || !BATCH) ? __float_as_uint(Dc[r]) : MARK_ADJ,
-                             (AFF || (BATCH && !own)) ? MARK_ADJ : __float_as_uint(Dn[r]));
+                        push((own || (zgr && glane_yz)) && Lp[r] != Lc[r], Lp[r], Lc[r],
+                             (own || !BATCH) ? __float_as_uint(Dp[r]) : MARK_ADJ,
+                             (AFF || (BATCH && !own)) ? MARK_ADJ : __float_as_uint(Dc[r]));
                     }
                 }
             }
@@ -848,6 +801,11 @@ __global__ __launch_bounds__(SCAN_THREADS, 4) void k_face_scan(ScanParams P, Rec
         // issued -- a wait placed after them (where the compiler would put it
         // on first use) would drain the new prefetch too
         __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
+#pragma unroll
+        for (int r = 0; r < ROWS; ++r) {
+            Lp[r] = Lc[r];
+            Dp[r] = Dc[r];
+        }
 #pragma unroll
         for (int r = 0; r <= ROWS; ++r) {
             Lc[r] = narrow(Ln[r]);
