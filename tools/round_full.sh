@@ -1,7 +1,7 @@
 #!/bin/bash
 # Full GPU suite, smoke, default bench line and every BASELINE config line.
 set -o pipefail
-TAG=${1:-r2h}
+TAG=${1:-full}
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 O=gpurun_out/$TAG
 mkdir -p $O
