@@ -79,6 +79,9 @@ PROTOTYPES = {
     'ctg_synth_volume': (ctypes.c_int, [c_vp, c_vp, c_vp, ctypes.c_int64, c_vp, ctypes.c_int, ctypes.c_uint64,
                                         ctypes.c_uint64, ctypes.c_double, c_vp]),
     'ctg_synth_affinities': (ctypes.c_int, [c_vp, c_vp, c_vp, ctypes.c_int, c_vp, c_vp]),
+    'ctg_filter_conv_axis': (ctypes.c_int, [c_vp, c_vp, c_vp, ctypes.c_int, ctypes.c_int, c_vp, ctypes.c_int, c_vp]),
+    'ctg_filter_combine': (ctypes.c_int, [ctypes.c_int, c_vp, c_vp, c_vp, c_vp, ctypes.c_int64, c_vp]),
+    'ctg_sym_eigenvalues': (ctypes.c_int, [c_vp, ctypes.c_int, ctypes.c_int64, c_vp, c_vp]),
     'ctg_trim': (ctypes.c_int, []),
     'ctg_io_read_box': (ctypes.c_int, [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                        c_vp, c_vp, ctypes.c_int, c_vp, c_vp, c_vp, ctypes.c_int]),

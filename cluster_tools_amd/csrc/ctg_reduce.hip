@@ -339,8 +339,12 @@ __global__ __launch_bounds__(256) void k_reduce_edges(int64_t E, const uint32_t*
         }
         const double c = (double)cnt;
         const double mean = sum / c;
+        // population variance from the f64 power sums: absolute error below
+        // ~(n + 2) eps max(x^2) (each x^2 of a float is exact in f64, the
+        // error is the accumulation's); an edge whose samples are all equal
+        // (min == max) has variance exactly 0, as the two-pass rule gives
         double var = (sq - sum * mean) / c;
-        if (var < 0.0) var = 0.0;
+        if (var < 0.0 || mn == mx) var = 0.0;
         const double vmin = (double)ord2f(mn), vmax = (double)ord2f(mx);
         double qv[5] = {0.0, 0.0, 0.0, 0.0, 0.0};   // registers (constant indices after unrolling)
         if (!(O.ablate & 1)) vigra_quantiles_cross(h, c, vmin, vmax, scale, offset, qv);

@@ -532,6 +532,9 @@ __global__ __launch_bounds__(SCAN_THREADS, 4) void k_face_scan(ScanParams P, Rec
     const bool g_x_lo = batch && inx && x >= gbx && x < gex;
     const bool glane_xf = g_x_lo && x + 1 < gex;
     const bool glane_yz = g_x_lo;
+    // the same lane sets as wave masks (uniform)
+    const uint64_t m_xf = __builtin_amdgcn_ballot_w64(lane_xf), m_yz = __builtin_amdgcn_ballot_w64(lane_yz);
+    const uint64_t m_gxf = __builtin_amdgcn_ballot_w64(glane_xf), m_gyz = __builtin_amdgcn_ballot_w64(glane_yz);
     // row masks (uniform): bit r for row y = yw + r
     uint32_t row_x = 0, row_y = 0, grow_x = 0, grow_y = 0;
 #pragma unroll
@@ -642,10 +645,11 @@ __global__ __launch_bounds__(SCAN_THREADS, 4) void k_face_scan(ScanParams P, Rec
         }
     };
     // append the active lanes of one site to the stage
-    auto push = [&](bool act, uint32_t a, uint32_t b, uint32_t za, uint32_t zb) {
+    // (the ballot is taken at the call site, PUSH below: through a bool
+    // parameter the compiler rebuilds the lane mask with a cndmask + compare)
+    auto push_m = [&](uint64_t m, bool act, uint32_t a, uint32_t b, uint32_t za, uint32_t zb) {
         // no early-out on an empty ballot: at ~15 % face density a site is
         // almost never empty, and k = 0 makes the rest a no-op
-        const uint64_t m = __builtin_amdgcn_ballot_w64(act);
         const int k = __popcll(m);
         if (nbuf + k > STAGE_CAP) flush_stage();
         const int rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
@@ -656,6 +660,14 @@ __global__ __launch_bounds__(SCAN_THREADS, 4) void k_face_scan(ScanParams P, Rec
         }
         nbuf += k;
     };
+    // PUSH(face compare, uniform 64-bit mask of the lanes whose face counts,
+    // per-lane membership, entry...): the ballot of the bare compare is the
+    // v_cmp result itself; and-ing the uniform lane mask is one scalar op
+#define PUSH(cmp, lanes, member, ...)                                      \
+    do {                                                                   \
+        const bool c_ = (cmp);                                             \
+        push_m(__builtin_amdgcn_ballot_w64(c_) & (lanes), c_ && (member), __VA_ARGS__); \
+    } while (0)
 
     // z faces are visited at their upper voxel's plane: a tile owns the faces
     // (z-1, z) for z in [z0, z1), so it starts from plane z0 - 1 (kept as the
@@ -685,6 +697,15 @@ __global__ __launch_bounds__(SCAN_THREADS, 4) void k_face_scan(ScanParams P, Rec
         const bool zup = z > 0 && zlo;                          // face (z-1, z): upper voxel in the own box
         const bool zg = batch && z >= gbz && z < gez;            // graph box planes (batched)
         const bool gzup = zg && z - 1 >= gbz;
+        // this plane's face sites as scalar bit masks (bit r = row r): owned x /
+        // y / z faces and (batched) graph-box faces -- tested with scalar bit
+        // tests, not carried as per-lane booleans
+        const uint32_t s_xo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(zlo ? row_x : 0u));
+        const uint32_t s_yo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(zlo ? row_y : 0u));
+        const uint32_t s_zo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(zup ? row_x : 0u));
+        const uint32_t s_xg = (uint32_t)__builtin_amdgcn_readfirstlane((int)(zg ? grow_x : 0u));
+        const uint32_t s_yg = (uint32_t)__builtin_amdgcn_readfirstlane((int)(zg ? grow_y : 0u));
+        const uint32_t s_zg = (uint32_t)__builtin_amdgcn_readfirstlane((int)(gzup ? grow_x : 0u));
         if (ablate & 8) {   // diagnostic: loads only
             uint32_t chk = 0;
 #pragma unroll
@@ -698,21 +719,22 @@ __global__ __launch_bounds__(SCAN_THREADS, 4) void k_face_scan(ScanParams P, Rec
                 const uint32_t lx = shl1(lc, (uint32_t)__builtin_amdgcn_readlane((int)XLc, r));
                 // owned faces carry samples; (batched) sub-graph faces the block
                 // does not own go in as adjacency-only entries
-                const bool xo = zlo && (row_x >> r & 1u), xg = zg && (grow_x >> r & 1u);
+                const bool xo = (s_xo >> r) & 1u, xg = BATCH && ((s_xg >> r) & 1u);
                 if ((xo || xg) && (!AFF || adj_marks)) {
                     const float dx = BND ? __uint_as_float(shl1(__float_as_uint(Dc[r]),
                                                                 (uint32_t)__builtin_amdgcn_readlane(
                                                                     (int)__float_as_uint(XDc), r)))
                                          : 0.f;
                     const bool own = xo && lane_xf;
-                    push((own || (xg && glane_xf)) && lc != lx, lc, lx, (own || !BATCH) ? __float_as_uint(Dc[r]) : MARK_ADJ,
+                    PUSH(lc != lx, (xo ? m_xf : 0ull) | (xg ? m_gxf : 0ull), own || (xg && glane_xf), lc, lx, (own || !BATCH) ? __float_as_uint(Dc[r]) : MARK_ADJ,
                          (AFF || (BATCH && !own)) ? MARK_ADJ : __float_as_uint(dx));
                 }
                 // y face (y, y+1)
-                const bool yo = zlo && (row_y >> r & 1u), yg = zg && (grow_y >> r & 1u);
+                const bool yo = (s_yo >> r) & 1u, yg = BATCH && ((s_yg >> r) & 1u);
                 if ((yo || yg) && (!AFF || adj_marks)) {
                     const bool own = yo && lane_yz;
-                    push((own || (yg && glane_yz)) && lc != Lc[r + 1], lc, Lc[r + 1],
+                    PUSH(lc != Lc[r + 1], (yo ? m_yz : 0ull) | (yg ? m_gyz : 0ull), own || (yg && glane_yz), lc,
+                         Lc[r + 1],
                          (own || !BATCH) ? __float_as_uint(Dc[r]) : MARK_ADJ,
                          (AFF || (BATCH && !own)) ? MARK_ADJ : __float_as_uint(Dc[r + 1]));
                 }
@@ -774,19 +796,20 @@ __global__ __launch_bounds__(SCAN_THREADS, 4) void k_face_scan(ScanParams P, Rec
                             const uint32_t mk = (P.bloom != nullptr && !(glr >> j & 1u)) ? MARK_ONE_ADJ : MARK_ONE;
 #pragma unroll
                             for (int r = 0; r < ROWS; ++r)
-                                push(act[j * ROWS + r], Lc[r], lq[j * ROWS + r], __float_as_uint(av[j * ROWS + r]), mk);
+                                PUSH(act[j * ROWS + r], ~0ull, true, Lc[r], lq[j * ROWS + r], __float_as_uint(av[j * ROWS + r]), mk);
                         }
                     }
                 }
             }
             // z faces (z-1, z): the previous plane against plane z
-            if ((zup || gzup) && (!AFF || adj_marks)) {
+            if ((s_zo | s_zg) && (!AFF || adj_marks)) {
 #pragma unroll
                 for (int r = 0; r < ROWS; ++r) {
-                    const bool zo = zup && (row_x >> r & 1u), zgr = gzup && (grow_x >> r & 1u);
+                    const bool zo = (s_zo >> r) & 1u, zgr = BATCH && ((s_zg >> r) & 1u);
                     if (zo || zgr) {
                         const bool own = zo && lane_yz;
-                        push((own || (zgr && glane_yz)) && Lp[r] != Lc[r], Lp[r], Lc[r],
+                        PUSH(Lp[r] != Lc[r], (zo ? m_yz : 0ull) | (zgr ? m_gyz : 0ull), own || (zgr && glane_yz),
+                             Lp[r], Lc[r],
                              (own || !BATCH) ? __float_as_uint(Dp[r]) : MARK_ADJ,
                              (AFF || (BATCH && !own)) ? MARK_ADJ : __float_as_uint(Dc[r]));
                     }
@@ -814,6 +837,7 @@ __global__ __launch_bounds__(SCAN_THREADS, 4) void k_face_scan(ScanParams P, Rec
         XLc = narrow(XLn);
         XDc = XDn;
     }
+#undef PUSH
     if (__ballot(ovf != 0) && lane == 0) atomicAdd(&C->label_overflow, 1ull);
     flush_stage();
     poll();

@@ -634,10 +634,42 @@ def extractBlockFeaturesFromAffinityMaps_uint8(graphPath, subgraphKey, dataPath,
                     outKey, halo_lo, halo_hi, off.tolist(), True, np.dtype(np.uint8))
 
 
+def accumulateInput(graph, input, labels, ignoreLabel, withSize, minVal, maxVal):  # noqa: N802,N803,A002
+    """ndist.accumulateInput (features/block_edge_features.py:159-168): the
+    per-edge statistics of a filter response over the faces of ``labels``
+    (both voxels of every boundary face, as the boundary-map features), for
+    the edges of ``graph`` in its uvIds order.  Histogram range [minVal,
+    maxVal] (the response's own min / max at the call site); columns mean,
+    var, min, q10, q25, q50, q75, q90, max (+ count when ``withSize``); an
+    edge of the graph with no face in ``labels`` gets a zero row.  One GPU
+    face scan (libctg.so) per call.  Column set and empty-edge rows: nifty's
+    accumulateInput is not in the image -- parity unpinned."""
+    uv = graph.uvIds() if hasattr(graph, 'uvIds') else np.asarray(graph, dtype=np.uint64).reshape(-1, 2)
+    uv = np.asarray(uv, dtype=np.uint64).reshape(-1, 2)
+    lab = np.ascontiguousarray(np.asarray(labels, dtype=np.uint64))
+    x = np.ascontiguousarray(np.asarray(input, dtype=np.float32))
+    if lab.shape != x.shape:
+        raise RuntimeError('accumulateInput: input shape %s != labels shape %s' % (x.shape, lab.shape))
+    lo, hi = float(minVal), float(maxVal)
+    if not hi > lo:                      # constant response: a unit range keeps the binning defined
+        hi = lo + 1.0
+    n_cols = N_FEATURES if withSize else N_FEATURES - 1
+    out = np.zeros((uv.shape[0], n_cols), dtype=np.float64)
+    if uv.shape[0] == 0 or lab.size == 0:
+        return out
+    r = rag.rag_features(lab, x, ignore_label=bool(ignoreLabel), hist_range=(lo, hi))
+    if r['edges'].shape[0]:
+        pos = rag.map_edge_ids(r['edges'], uv)
+        hit = pos >= 0
+        out[hit] = r['features'][pos[hit], :n_cols]
+    return out
+
+
 def mergeFeatureBlocks(graphPath, subgraphKey, featuresPath, featuresKey, outPath, outKey,  # noqa: N802,N803
                        blockIds, edgeIdBegin, edgeIdEnd, numberOfThreads=1):  # noqa: N803
     """Combine the per-block feature rows of edges in [edgeIdBegin, edgeIdEnd)
-    into rows of the (E,10) ``outKey`` dataset.
+    into rows of the (E, n_features) ``outKey`` dataset (10 columns, or
+    9 k + 1 for the filter-feature branch).
 
     Blocks written by this library carry the mergeable statistics in the
     ``<featuresKey>_stats`` companion (uint32, 52 words per edge): counts and
@@ -656,7 +688,8 @@ def mergeFeatureBlocks(graphPath, subgraphKey, featuresPath, featuresKey, outPat
         ds_ids = g['edge_ids']
         have_stats = featuresKey + STATS_SUFFIX in ff
         ds_feat = ff[featuresKey + STATS_SUFFIX] if have_stats else ff[featuresKey]
-        width = STATS_WORDS if have_stats else N_FEATURES
+        n_features = int(ff[featuresKey].attrs.get('n_features', N_FEATURES))
+        width = STATS_WORDS if have_stats else n_features
 
         block_ids = [int(b) for b in blockIds]
         positions = [blk.blockGridPosition(b) for b in block_ids]
@@ -673,7 +706,7 @@ def mergeFeatureBlocks(graphPath, subgraphKey, featuresPath, featuresKey, outPat
             sel = (ids >= begin) & (ids < end)
             if sel.any():
                 parts.append((ids[sel], rows[sel]))
-    out = np.zeros((end - begin, N_FEATURES), np.float64)
+    out = np.zeros((end - begin, N_FEATURES if have_stats else n_features), np.float64)
     if parts:
         ids = np.concatenate([p[0] for p in parts]).astype(np.uint64)
         rows = np.concatenate([p[1] for p in parts], axis=0)
@@ -684,7 +717,19 @@ def mergeFeatureBlocks(graphPath, subgraphKey, featuresPath, featuresKey, outPat
             recs[:, 42] |= np.uint32(0x80000000)   # every block row is a graph edge
             merged = rag.merge_stats(keys, sums, recs)
             out[merged['edges'][:, 1].astype(np.int64) - begin] = merged['features']
-        else:
+        elif n_features == N_FEATURES:
             out = rag.merge_feature_rows(ids, rows, begin, end)
+        else:
+            # filter features (block_edge_features.py:226-233): groups of 9
+            # statistics per (filter, sigma, channel) and the size column
+            # last; each group merges as a 10-column row with that size
+            if (n_features - 1) % (N_FEATURES - 1):
+                raise RuntimeError('mergeFeatureBlocks: %d feature columns are not 9 k + 1' % n_features)
+            size = rows[:, -1:]
+            for g in range((n_features - 1) // (N_FEATURES - 1)):
+                cols = slice(g * (N_FEATURES - 1), (g + 1) * (N_FEATURES - 1))
+                m = rag.merge_feature_rows(ids, np.concatenate([rows[:, cols], size], axis=1), begin, end)
+                out[:, cols] = m[:, :N_FEATURES - 1]
+                out[:, -1] = m[:, -1]
     with _open(outPath) as fo:
         fo[outKey][begin:end, :] = out

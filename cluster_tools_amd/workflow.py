@@ -11,7 +11,8 @@ library (its calls are serialised per device) and overlap their N5 decode.
     InitialSubGraphs   initial_sub_graphs.py:49-90, job :134-157
     MergeSubGraphs     merge_sub_graphs.py:52-96, job :155-195 (complete graph)
     MapEdgeIds         map_edge_ids.py:36-70, job :101-120
-    BlockEdgeFeatures  block_edge_features.py:48-87, job :275-327 (_accumulate)
+    BlockEdgeFeatures  block_edge_features.py:48-87, job :275-327 (_accumulate, and the
+                       filter branch _accumulate_with_filters :151-272 on the GPU filters)
     MergeEdgeFeatures  merge_edge_features.py:35-84, job :110-149
 
 This is what bench.py's ``--config 0`` times (BASELINE configs[0]) and what
@@ -25,8 +26,8 @@ from concurrent.futures import ThreadPoolExecutor
 
 import numpy as np
 
-from . import ndist
-from .blocking import blocks_in_volume
+from . import fastfilters, ndist
+from .blocking import blocking, blocks_in_volume
 
 
 def _jobs(block_list, n_jobs):
@@ -35,12 +36,11 @@ def _jobs(block_list, n_jobs):
 
 
 def _run_jobs(fn, jobs):
+    """Run the job bodies (threads); their return values in job order."""
     if len(jobs) == 1:
-        fn(jobs[0])
-        return
+        return [fn(jobs[0])]
     with ThreadPoolExecutor(len(jobs)) as ex:
-        for f in [ex.submit(fn, j) for j in jobs]:
-            f.result()
+        return [f.result() for f in [ex.submit(fn, j) for j in jobs]]
 
 
 class Timer:
@@ -103,11 +103,76 @@ def graph_workflow(input_path, input_key, graph_path, output_key, block_shape, m
     return timer
 
 
+def _normalize(x):
+    """vu.normalize (utils/volume_utils.py:98-105): float32, min to 0, max to 1."""
+    x = np.asarray(x, dtype=np.float32).copy()
+    x -= x.min()
+    m = x.max()
+    if m > 0:
+        x /= m
+    return x
+
+
+def _accumulate_filter(input_, graph, labels, bb_local, filter_name, sigma, ignore_label, with_size, apply_in_2d):
+    """block_edge_features.py:151-168: filter response on the GPU, then one
+    accumulateInput per response channel (size column on the last one)."""
+    response = fastfilters.apply_filter(input_, filter_name, sigma, apply_in_2d=apply_in_2d)[bb_local]
+    if response.ndim == 4:
+        n_chan = response.shape[-1]
+        return np.concatenate([ndist.accumulateInput(graph, response[..., c], labels, ignore_label,
+                                                     with_size and c == n_chan - 1,
+                                                     response[..., c].min(), response[..., c].max())
+                               for c in range(n_chan)], axis=1)
+    return ndist.accumulateInput(graph, response, labels, ignore_label, with_size, response.min(), response.max())
+
+
+def _filter_block(block_id, blk, ds_in, ds_labels, ds_edges, ds_out, filters, sigmas, halo, ignore_label,
+                  apply_in_2d, channel_agglomeration):
+    """block_edge_features.py:171-238 (_accumulate_block): the block's
+    sub-graph, its labels over the inner block + 1 (positive side), the
+    normalised input with the filter halo; one row block of
+    len(filters) x len(sigmas) x 9 (+ size) columns per edge."""
+    pos = blk.blockGridPosition(block_id)
+    edges = ds_edges.read_chunk(pos)
+    if edges is None:
+        return None
+    graph = ndist.Graph(np.asarray(edges).reshape(-1, 2))
+    shape = ds_labels.shape
+    if sum(halo) > 0:
+        b = blk.getBlockWithHalo(block_id, list(halo))
+        bshape = b.outerBlock.shape
+        bb_in = tuple(slice(x, y) for x, y in zip(b.outerBlock.begin, b.outerBlock.end))
+        bb = tuple(slice(x, min(y + 1, sh)) for x, y, sh in zip(b.innerBlock.begin, b.innerBlock.end, shape))
+        bb_local = tuple(slice(x, min(y + 1, bs)) for x, y, bs in
+                         zip(b.innerBlockLocal.begin, b.innerBlockLocal.end, bshape))
+    else:
+        b = blk.getBlock(block_id)
+        bb = tuple(slice(x, min(y + 1, sh)) for x, y, sh in zip(b.begin, b.end, shape))
+        bb_in = bb
+        bb_local = slice(None)
+    if ds_in.ndim == 4:
+        bb_in = (slice(0, 3),) + bb_in
+    input_ = _normalize(ds_in[bb_in])
+    if ds_in.ndim == 4:
+        if channel_agglomeration is None:
+            raise ValueError('4-D filter input needs a channel_agglomeration')
+        input_ = getattr(np, channel_agglomeration)(input_, axis=0)
+    labels = ds_labels[bb]
+    feats = [_accumulate_filter(input_, graph, labels, bb_local, f, s, ignore_label,
+                                f == filters[-1] and s == sigmas[-1], apply_in_2d)
+             for f in filters for s in sigmas]
+    feats = np.concatenate(feats, axis=1)
+    ds_out.write_chunk(pos, feats.flatten(), True)
+    return feats.shape[1]
+
+
 def edge_features_workflow(input_path, input_key, labels_path, labels_key, graph_path, graph_key, output_path,
                            output_key, block_shape, max_jobs=1, max_jobs_merge=1, threads_per_job=16, offsets=None,
-                           timer=None):
+                           timer=None, filters=None, sigmas=None, halo=(0, 0, 0), apply_in_2d=False,
+                           channel_agglomeration='mean'):
     """EdgeFeaturesWorkflow: per-block features into s0/sub_features, merged
-    (E, 10) table at ``output_key``."""
+    (E, n_features) table at ``output_key``; ``filters`` / ``sigmas`` select
+    the filter-feature branch (block_edge_features.py:297-319)."""
     timer = timer or Timer()
     with ndist._open(graph_path, 'r') as f:
         shape = list(f['s0/sub_graphs'].attrs['shape'])
@@ -123,6 +188,22 @@ def edge_features_workflow(input_path, input_key, labels_path, labels_key, graph
             ds.attrs['n_features'] = 10                           # :321-325
 
         def job(blocks):                                          # block_edge_features.py:113-148
+            if filters is not None:                               # :304-319, _accumulate_with_filters
+                if offsets is not None:
+                    raise ValueError('Filters and offsets are not supported')   # :310
+                if sigmas is None:
+                    raise ValueError('Need sigma values')                       # :312
+                with ndist._open(input_path, 'r') as fi, ndist._open(labels_path, 'r') as fl, \
+                        ndist._open(graph_path, 'r') as fg, ndist._open(output_path) as fo:
+                    g = fg['s0/sub_graphs']
+                    blk = blocking([0, 0, 0], list(g.attrs['shape']), list(block_shape))
+                    n = None
+                    for b in blocks:
+                        r = _filter_block(b, blk, fi[input_key], fl[labels_key], g['edges'], fo['s0/sub_features'],
+                                          filters, sigmas, halo, bool(g.attrs['ignore_label']), apply_in_2d,
+                                          channel_agglomeration)
+                        n = r if r is not None else n
+                return n
             if ndim == 3:
                 fn = ndist.extractBlockFeaturesFromBoundaryMaps_uint8 if dtype == np.uint8 else \
                     ndist.extractBlockFeaturesFromBoundaryMaps_float32
@@ -133,12 +214,16 @@ def edge_features_workflow(input_path, input_key, labels_path, labels_key, graph
                     ndist.extractBlockFeaturesFromAffinityMaps_float32
                 fn(graph_path, 's0/sub_graphs', input_path, input_key, labels_path, labels_key, blocks,
                    output_path, 's0/sub_features', offsets)
-        _run_jobs(job, _jobs(block_list, max_jobs))
+            return 10
+        n_feats = [n for n in _run_jobs(job, _jobs(block_list, max_jobs)) if n is not None]
+        n_features = n_feats[0] if n_feats else 10
+        with ndist._open(output_path) as f:                     # job 0 writes n_features (:321-325)
+            f['s0/sub_features'].attrs['n_features'] = int(n_features)
     with timer.stage('merge_edge_features'):
         chunk = min(262144, n_edges)
         with ndist._open(output_path) as f:                     # merge_edge_features.py:62-65
-            f.require_dataset(output_key, shape=(n_edges, 10), chunks=(max(1, chunk), 1), compression='gzip',
-                              dtype='float64')
+            f.require_dataset(output_key, shape=(n_edges, n_features), chunks=(max(1, chunk), 1),
+                              compression='gzip', dtype='float64')
         # edge chunks of chunk_size dealt to the merge jobs as consecutive runs
         # (merge_edge_features.py:74-79, cluster_tasks.py:305-329); one
         # mergeFeatureBlocks call per job over its run (:127-147)

@@ -190,6 +190,19 @@ void ctg_free(ctg_result* r);
 int ctg_synth_volume(uint64_t* labels, float* boundary, const int64_t* shape,
                      int64_t z_offset, const int64_t* global_shape, int cell,
                      uint64_t seed, uint64_t label_offset, double noise_amp, void* stream);
+/* Filter-feature branch (features/block_edge_features.py:151-238): the
+ * fastfilters / vigra filters vu.apply_filter runs (utils/volume_utils.py:80-94),
+ * on device float32 arrays (cluster_tools_amd/fastfilters.py).
+ * ctg_filter_conv_axis: out[p] = sum_k taps[k] in[reflect(p + (k - n_taps/2) e_axis)],
+ *   C-order shape[ndim] (ndim <= 3), odd n_taps <= 257, mirror borders. */
+int ctg_filter_conv_axis(const float* in, float* out, const int64_t* shape, int ndim, int axis, const float* taps,
+                         int n_taps, void* stream);
+/* op 0: sqrt(a^2+b^2+c^2), 1: a+b+c (b, c may be NULL), 2: a*b, 3: a-b; n elements */
+int ctg_filter_combine(int op, const float* a, const float* b, const float* c, float* out, int64_t n, void* stream);
+/* eigenvalues (descending) of n symmetric dim x dim matrices (dim 2 or 3), upper-triangle
+ * components as planes comps[k*n + i]; out (n, dim) */
+int ctg_sym_eigenvalues(const float* comps, int dim, int64_t n, float* out, void* stream);
+
 int ctg_synth_affinities(const float* boundary, float* affs, const int64_t* shape,
                          int n_channels, const int32_t* offsets, void* stream);
 
