@@ -105,12 +105,24 @@ __device__ __forceinline__ void entry_reset(Table& T, int e) {
 }
 
 // home bucket: four slots starting at a multiple of 4, read by two ds_read_b128
+// Two full-rate 24-bit multiplies (v_mul_u32_u24) instead of 32-bit ones and a
+// 64-bit multiply-add: bits 14.. of the product sum mix every one of the low
+// 24 bits of u and v; labels that differ only above bit 24 share buckets,
+// which costs probes, never correctness.
+#ifndef CTG_HASH24
+#define CTG_HASH24 1
+#endif
 __device__ __forceinline__ uint32_t home_bucket(uint32_t u, uint32_t v) {
+#if CTG_HASH24
+    const uint32_t p = (u & 0xFFFFFFu) * 0x9E3779u + ((v ^ (u >> 24)) & 0xFFFFFFu) * 0x85EBCBu;
+    return (p >> 12) & (TABLE_CAP - 4);
+#else
     uint32_t h = u * 0x9E3779B1u + v * 0x85EBCA6Bu;
     h ^= h >> 15;
     h *= 0x2C1B3C6Du;
     h ^= h >> 13;
     return h & (TABLE_CAP - 4);
+#endif
 }
 
 // Workgroup barrier that orders LDS only.  __syncthreads() also waits for every
