@@ -64,6 +64,9 @@ constexpr int STAGE_CAP = WAVE * NPER;                    // stage entries per w
 // u16 histogram slots: a table entry holds at most 65535 samples.  Each wave
 // folds at most this many samples between two table flushes (it requests a
 // flush before a batch would exceed it), so no entry can pass the bound.
+// u16 histogram slots: a table entry holds at most 65535 samples.  Each wave
+// folds at most this many samples between two table flushes (it requests a
+// flush before a batch would exceed it), so no entry can pass the bound.
 constexpr uint32_t WAVE_SAMPLE_BUDGET = 65535u / WAVES;
 #ifndef CTG_FILL_SOFT
 #define CTG_FILL_SOFT (TABLE_CAP / 2)
@@ -139,7 +142,10 @@ __device__ __forceinline__ void lds_barrier() {
 // table slots (entry tid) - its own record range from one global atomic, its
 // own 128-byte bodies, its own resets - so the flush needs two workgroup
 // barriers (table stable / table empty) instead of a workgroup-wide
-// compaction with one serial record reservation.
+// compaction with one serial record reservation.  (Tried: keeping entries
+// touched in the planes the waves still work on across a flush -- at a
+// 512-entry table nearly every live entry is that recent, and records did not
+// drop.)
 template <int MODE>
 __device__ __noinline__ void table_flush_waves(Table& T, RecordBuf R, Counters* C) {
     static_assert(TABLE_CAP == SCAN_THREADS, "one table entry per thread in the flush");
@@ -151,12 +157,12 @@ __device__ __noinline__ void table_flush_waves(Table& T, RecordBuf R, Counters* 
         T.flush_req = 0;
     }
     const uint64_t k = T.key[tid];
-    const bool live = k != EMPTY_KEY;
-    const uint64_t m = __ballot(live);
+    const bool out = k != EMPTY_KEY;
+    const uint64_t m = __ballot(out);
     if (m) {
         const uint32_t n = (uint32_t)__popcll(m);
         const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
-        uint32_t mv = live ? (uint32_t)k : 0u;
+        uint32_t mv = out ? (uint32_t)k : 0u;
         for (int o = 32; o > 0; o >>= 1) mv = max(mv, (uint32_t)__shfl_xor((int)mv, o, WAVE));
         const int reg = (blockIdx.x * WAVES + wv) & (NREG - 1);
         unsigned long long b = 0;
@@ -168,7 +174,7 @@ __device__ __noinline__ void table_flush_waves(Table& T, RecordBuf R, Counters* 
                                         (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)b);
         const unsigned long long rcap = (unsigned long long)R.rcap, slot0 = (unsigned long long)reg * rcap + base;
         uint16_t* cw = T.compact + wv * WAVE;
-        if (live) {
+        if (out) {
             if (base + rank < rcap) R.key[slot0 + rank] = k;
             cw[rank] = (uint16_t)tid;
         }
@@ -202,7 +208,7 @@ __device__ __noinline__ void table_flush_waves(Table& T, RecordBuf R, Counters* 
             }
         }
         __builtin_amdgcn_wave_barrier();
-        if (live) entry_reset(T, tid);
+        if (out) entry_reset(T, tid);
     }
     lds_barrier();
 }
@@ -570,10 +576,6 @@ __global__ __launch_bounds__(SCAN_THREADS, 4) void k_face_scan(ScanParams P, Rec
     uint32_t Lc[ROWS + 1];
     LabelT Ln[ROWS + 1];
     float Dc[ROWS + 1], Dn[ROWS + 1];
-    // previous plane (rows 0..ROWS-1): z faces pair plane z-1 with plane z,
-    // so a plane's faces never wait on the plane being prefetched
-    uint32_t Lp[ROWS];
-    float Dp[ROWS];
     uint32_t XLc = 0;
     LabelT XLn = 0;
     float XDc = 0.f, XDn = 0.f;
@@ -681,20 +683,8 @@ __global__ __launch_bounds__(SCAN_THREADS, 4) void k_face_scan(ScanParams P, Rec
         push_m(__builtin_amdgcn_ballot_w64(c_) & (lanes), c_ && (member), __VA_ARGS__); \
     } while (0)
 
-    // z faces are visited at their upper voxel's plane: a tile owns the faces
-    // (z-1, z) for z in [z0, z1), so it starts from plane z0 - 1 (kept as the
-    // previous plane only)
-    const bool has_prev = z0 > 0;
     if (z0 < z1) {
-        load_plane(has_prev ? z0 - 1 : z0, Ln, Dn, XLn, XDn);
-        __builtin_amdgcn_s_waitcnt(0x0F70);
-#pragma unroll
-        for (int r = 0; r < ROWS; ++r) {
-            Lp[r] = narrow(Ln[r]);
-            Dp[r] = Dn[r];
-        }
         load_plane(z0, Ln, Dc, XLn, XDc);
-        __builtin_amdgcn_s_waitcnt(0x0F70);
 #pragma unroll
         for (int r = 0; r <= ROWS; ++r) Lc[r] = narrow(Ln[r]);
         XLc = narrow(XLn);
@@ -703,12 +693,16 @@ __global__ __launch_bounds__(SCAN_THREADS, 4) void k_face_scan(ScanParams P, Rec
     for (int z = z0; z < z1; ++z) {
         const bool hz = z + 1 < Z;
         // prefetch of plane z + 1, unconditional (the last plane re-reads
-        // itself): in flight during all of plane z's faces
+        // itself; its z faces are masked by hz): in flight during the x / y
+        // faces, consumed by the z faces (z, z+1) at the end of the plane.
+        // (Tried: z faces (z-1, z) against the previous plane, so nothing in
+        // a plane waits for the prefetch -- 0.006 ms faster at 512^3, but the
+        // changed face order raised records by 23 % at cell 5.)
         load_plane(hz ? z + 1 : z, Ln, Dn, XLn, XDn);
         const bool zlo = z >= obz && z < oez;
-        const bool zup = z > 0 && zlo;                          // face (z-1, z): upper voxel in the own box
+        const bool zup = hz && z + 1 >= obz && z + 1 < oez;      // face (z, z+1): upper voxel in the own box
         const bool zg = batch && z >= gbz && z < gez;            // graph box planes (batched)
-        const bool gzup = zg && z - 1 >= gbz;
+        const bool gzup = zg && z + 1 < gez;
         // this plane's face sites as scalar bit masks (bit r = row r): owned x /
         // y / z faces and (batched) graph-box faces -- tested with scalar bit
         // tests, not carried as per-lane booleans
@@ -813,17 +807,17 @@ __global__ __launch_bounds__(SCAN_THREADS, 4) void k_face_scan(ScanParams P, Rec
                     }
                 }
             }
-            // z faces (z-1, z): the previous plane against plane z
+            // z faces (z, z+1): plane z against the prefetched plane
             if ((s_zo | s_zg) && (!AFF || adj_marks)) {
 #pragma unroll
                 for (int r = 0; r < ROWS; ++r) {
                     const bool zo = (s_zo >> r) & 1u, zgr = BATCH && ((s_zg >> r) & 1u);
                     if (zo || zgr) {
                         const bool own = zo && lane_yz;
-                        PUSH(Lp[r] != Lc[r], (zo ? m_yz : 0ull) | (zgr ? m_gyz : 0ull), own || (zgr && glane_yz),
-                             Lp[r], Lc[r],
-                             (own || !BATCH) ? __float_as_uint(Dp[r]) : MARK_ADJ,
-                             (AFF || (BATCH && !own)) ? MARK_ADJ : __float_as_uint(Dc[r]));
+                        const uint32_t ln = (uint32_t)Ln[r];
+                        PUSH(Lc[r] != ln, (zo ? m_yz : 0ull) | (zgr ? m_gyz : 0ull), own || (zgr && glane_yz),
+                             Lc[r], ln, (own || !BATCH) ? __float_as_uint(Dc[r]) : MARK_ADJ,
+                             (AFF || (BATCH && !own)) ? MARK_ADJ : __float_as_uint(Dn[r]));
                     }
                 }
             }
@@ -836,11 +830,6 @@ __global__ __launch_bounds__(SCAN_THREADS, 4) void k_face_scan(ScanParams P, Rec
         // issued -- a wait placed after them (where the compiler would put it
         // on first use) would drain the new prefetch too
         __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
-#pragma unroll
-        for (int r = 0; r < ROWS; ++r) {
-            Lp[r] = Lc[r];
-            Dp[r] = Dc[r];
-        }
 #pragma unroll
         for (int r = 0; r <= ROWS; ++r) {
             Lc[r] = narrow(Ln[r]);
