@@ -334,14 +334,18 @@ __device__ __forceinline__ void fold_stats(Table& T, const StageT& e, int s, Rec
         // block does not own -- the key is inserted, no sample counted
         const bool adj = (AFF || BATCH) && e.w == MARK_ADJ && (AFF || e.z == MARK_ADJ);
         const uint32_t nnf = (AFF && e.w == MARK_ONE_ADJ) ? ADJ_FLAG : 0u;   // sample that proves adjacency
+        // affinity entries carry one sample (.w a marker) or, for two
+        // neighbouring lanes of one long-range channel with the same key, two
+        // samples (.w the second; the push never pairs a marker-valued sample)
+        const bool two = BND || (AFF && e.w < MARK_ONE_ADJ);
         const float a = __uint_as_float(e.z);
-        const float b = BND ? __uint_as_float(e.w) : a;
-        const uint32_t n = adj ? 0u : (BND ? 2u : 1u);
+        const float b = two ? __uint_as_float(e.w) : a;
+        const uint32_t n = adj ? 0u : (two ? 2u : 1u);
         const double da = (double)a, db = (double)b;
         const int sa = adj ? -1 : sample_slot<FAST40>(da, scale, offset);
-        const int sb = (BND && !adj) ? sample_slot<FAST40>(db, scale, offset) : -1;
-        const double ds = BND ? da + db : da;
-        const double dq = BND ? da * da + db * db : da * da;
+        const int sb = (two && !adj) ? sample_slot<FAST40>(db, scale, offset) : -1;
+        const double ds = two ? da + db : da;
+        const double dq = two ? da * da + db * db : da * da;
         const uint32_t mn = f2ord(fminf(a, b)), mx = f2ord(fmaxf(a, b));
         if (s < 0) {
             emit_direct(R, C, key, n | (adj ? ADJ_FLAG : nnf), sa, sb, adj ? 0.0 : ds, adj ? 0.0 : dq,
@@ -367,6 +371,7 @@ __device__ __forceinline__ void fold_stats(Table& T, const StageT& e, int s, Rec
         if (nnf) atomicOr(&T.w[s][21], ADJ_FLAG);
         if (ablate & 128) return;   // diagnostic: no histogram
         if constexpr (BND) hist_add2(T, s, sa, sb);
+        else if (two) hist_add2(T, s, sa, sb);
         else atomicAdd(&T.w[s][sa >> 1], 1u << ((sa & 1) * 16));
     }
 }
@@ -430,6 +435,11 @@ __device__ __forceinline__ uint64_t stamp_now() {
     uint64_t t;
     asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
     return t;
+}
+
+// lane pairs (2i, 2i+1) exchange a value (DPP quad_perm [1,0,3,2])
+__device__ __forceinline__ uint32_t swap1(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0xB1, 0xf, 0xf, false);
 }
 
 // x-neighbour of every lane: lane i gets lane i+1 (DPP wave_shl:1), lane 63
@@ -642,7 +652,7 @@ __global__ __launch_bounds__(SCAN_THREADS, 4) void k_face_scan(ScanParams P, Rec
         if (nbuf) {
             if constexpr (STATS) {
                 // per-wave sample budget: flush first if this batch would pass it
-                const uint32_t add = BND ? 2u * (uint32_t)nbuf : (uint32_t)nbuf;
+                const uint32_t add = (BND || AFF) ? 2u * (uint32_t)nbuf : (uint32_t)nbuf;   // AFF: paired entries
                 if (wsamp + add > WAVE_SAMPLE_BUDGET) {
                     need = true;
                     poll();
@@ -800,9 +810,29 @@ __global__ __launch_bounds__(SCAN_THREADS, 4) void k_face_scan(ScanParams P, Rec
                         for (int j = 0; j < AFF_G; ++j) {
                             if (c0 + j >= P.n_channels) break;
                             const uint32_t mk = (P.bloom != nullptr && !(glr >> j & 1u)) ? MARK_ONE_ADJ : MARK_ONE;
+                            if (mk == MARK_ONE) {
+                                // long-range (or unfiltered) channel: lanes 2i, 2i+1 with the
+                                // same key fold as one two-sample entry (along x a cell pair
+                                // spans runs of lanes), ~halving this channel's fold work
 #pragma unroll
-                            for (int r = 0; r < ROWS; ++r)
-                                PUSH(act[j * ROWS + r], ~0ull, true, Lc[r], lq[j * ROWS + r], __float_as_uint(av[j * ROWS + r]), mk);
+                                for (int r = 0; r < ROWS; ++r) {
+                                    const int k = j * ROWS + r;
+                                    const uint32_t sv = __float_as_uint(av[k]);
+                                    const uint32_t nq = swap1(lq[k]), ns = swap1(sv), nact = swap1(act[k] ? 1u : 0u);
+                                    const bool pair = act[k] && nact && nq == lq[k] && ns < MARK_ONE_ADJ &&
+                                                      sv < MARK_ONE_ADJ;   // Lc[r] is equal on the pair unless a face
+                                    const bool lead = (lane & 1) == 0;
+                                    const bool same_c = swap1(Lc[r]) == Lc[r];
+                                    const bool pr = pair && same_c;
+                                    PUSH(act[k] && !(pr && !lead), ~0ull, true, Lc[r], lq[k], sv,
+                                         (pr && lead) ? ns : MARK_ONE);
+                                }
+                            } else {
+#pragma unroll
+                                for (int r = 0; r < ROWS; ++r)
+                                    PUSH(act[j * ROWS + r], ~0ull, true, Lc[r], lq[j * ROWS + r],
+                                         __float_as_uint(av[j * ROWS + r]), mk);
+                            }
                         }
                     }
                 }
