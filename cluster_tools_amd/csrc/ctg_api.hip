@@ -26,6 +26,8 @@ hipError_t launch_pack_keys(int64_t n, const uint64_t* key, int nb, uint64_t* sk
 hipError_t launch_pack_regions(const uint64_t* key, int64_t rcap, const RegionPrefix& pre, int nb, int ib, uint64_t* sk,
                                uint32_t* idx, hipStream_t s);
 hipError_t launch_pack_pairs(int64_t n, const uint64_t* uv, int nb, uint64_t* sk, uint32_t* idx, hipStream_t s);
+hipError_t bucket_sort_keys(const uint64_t* keys, uint64_t* tmp, uint64_t* out, int64_t n, int lo_bit, int hi_bit,
+                            uint32_t* small, void** temp, size_t* temp_bytes, hipStream_t s);
 hipError_t launch_max_pairs(int64_t n, const uint64_t* uv, unsigned long long* out, hipStream_t s);
 hipError_t launch_reduce(int64_t E, const uint32_t* dE, const uint64_t* uniq, const uint32_t* runs,
                          const uint32_t* offs, const uint32_t* perm32, const uint64_t* perm64, int ib,
@@ -161,6 +163,8 @@ static hipError_t ws_init(Workspace& w) {
     if (e != hipSuccess) return e;
     e = hipMalloc(&w.small, 64 * sizeof(unsigned int));
     if (e != hipSuccess) return e;
+    e = hipMalloc(&w.bsort, (3 * 4096 + 1) * sizeof(uint32_t));   // bucket sort counts / offsets / cursors
+    if (e != hipSuccess) return e;
     e = hipHostMalloc(&w.small_host, 64 * sizeof(unsigned int), hipHostMallocDefault);
     if (e != hipSuccess) return e;
     for (int i = 0; i < 8; ++i) hipEventCreate(&w.ev[i]);
@@ -243,6 +247,10 @@ using RecordSortConfig = rocprim::default_config;
 // to this many records (CTG_SORT_WIDE_MAX overrides).
 static bool sort_packed() {
     const char* e = getenv("CTG_SORT_PACKED");   // read per call: tests switch it
+    return !(e && e[0] == '0');
+}
+static bool bucket_sort() {
+    const char* e = getenv("CTG_BUCKET_SORT");   // read per call: A/B and tests switch it
     return !(e && e[0] == '0');
 }
 static int64_t sort_wide_digits_max() {
@@ -333,7 +341,15 @@ static hipError_t reduce_records(Workspace& w, const ReduceJob& J, hipStream_t s
     else e = launch_pack_pairs(n, J.pairs, nb, w.sk_in, w.idx_in, s);
     if (e != hipSuccess) return e;
     ev.mark(2);
-    if (packed) {
+    if (packed && bucket_sort()) {
+        // MSD bucket pass + segmented sort of the key bits (ctg_sort.hip):
+        // 4 fused launches instead of 4 onesweep passes with their fills
+        e = bucket_sort_keys(w.sk_in, w.uniq, w.sk_out, n, ib, ib + ub + nb, w.bsort, &w.temp, &w.temp_bytes, s);
+        if (e != hipSuccess) return e;
+        ev.mark(3);
+        auto key_only = rocprim::make_transform_iterator(w.sk_out, [ib] __device__(uint64_t k) { return k >> ib; });
+        ROCPRIM_CALL(w, rocprim::run_length_encode(t, tbytes, key_only, (unsigned)n, w.uniq, w.runs, dE_all, s));
+    } else if (packed) {
         ROCPRIM_CALL(w, rocprim::radix_sort_keys<RecordSortConfig>(t, tbytes, w.sk_in, w.sk_out, (size_t)n,
                                                                    (unsigned)ib, (unsigned)(ib + ub + nb), s));
         ev.mark(3);

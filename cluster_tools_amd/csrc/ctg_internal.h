@@ -191,6 +191,7 @@ struct Workspace {
     Counters* counters_host = nullptr;   // pinned
     unsigned int* small = nullptr;       // device scalars (run counts etc.)
     unsigned int* small_host = nullptr;
+    uint32_t* bsort = nullptr;           // device: bucket-sort counts / offsets / cursors (ctg_sort.hip)
     // host->device staging of volumes
     void* stage[2] = {nullptr, nullptr};
     size_t stage_bytes[2] = {0, 0};

@@ -810,7 +810,10 @@ __global__ __launch_bounds__(SCAN_THREADS, 4) void k_face_scan(ScanParams P, Rec
                         for (int j = 0; j < AFF_G; ++j) {
                             if (c0 + j >= P.n_channels) break;
                             const uint32_t mk = (P.bloom != nullptr && !(glr >> j & 1u)) ? MARK_ONE_ADJ : MARK_ONE;
-                            if (mk == MARK_ONE) {
+#ifndef CTG_PAIR_ALL
+#define CTG_PAIR_ALL 0   // 1: pair nearest-neighbour channels too (A/B: nn1024 scan 8.6 -> 9.4 ms)
+#endif
+                            if (mk == MARK_ONE && (CTG_PAIR_ALL || P.bloom != nullptr)) {
                                 // long-range (or unfiltered) channel: lanes 2i, 2i+1 with the
                                 // same key fold as one two-sample entry (along x a cell pair
                                 // spans runs of lanes), ~halving this channel's fold work

@@ -1,0 +1,132 @@
+// Record-key sort for the back half (gfx950): MSD bucket pass + segmented sort.
+//
+// The scan's record keys (packed (u,v) with the record slot in the low ib
+// bits) come out of the face scan grouped by tile, and the reduction only
+// needs them grouped by key and ordered by (u,v).  rocPRIM's onesweep sorts
+// the 57-bit words of the 512^3 step in 4 passes of 10 bits, each a launch
+// with its own look-back state and buffer fills (~150 us at 2 M records: the
+// passes are launch- and latency-bound at that size).  Here:
+//
+//   k_bucket_hist    histogram of the top BB key bits (LDS per workgroup)
+//   k_bucket_scan    exclusive scan of the 2^BB counts (one workgroup)
+//   k_bucket_scatter every key to its bucket (per-workgroup LDS ranks, one
+//                    global reservation per (workgroup, bucket))
+//   rocprim::segmented_radix_sort_keys over the buckets, on the key bits below
+//                    the bucket bits only (the slot bits need no order)
+//
+// BB is chosen so a bucket averages ~1 K keys (LDS-sized segments); any skew
+// (e.g. one label adjacent to many: background) is handled by the segmented
+// sort's large-segment path, so there is no size precondition.
+#include <rocprim/device/device_segmented_radix_sort.hpp>
+
+#include "ctg_internal.h"
+
+namespace ctg {
+
+constexpr int BK_THREADS = 256;
+constexpr int BK_CHUNK = 4096;   // keys per workgroup in the histogram / scatter
+constexpr int BK_MAX_BITS = 12;  // at most 4096 buckets (LDS counters)
+
+__global__ __launch_bounds__(BK_THREADS) void k_bucket_hist(const uint64_t* __restrict__ keys, int64_t n, int shift,
+                                                            uint32_t nbk, uint32_t* __restrict__ counts) {
+    __shared__ uint32_t h[1 << BK_MAX_BITS];
+    for (uint32_t i = threadIdx.x; i < nbk; i += BK_THREADS) h[i] = 0;
+    __syncthreads();
+    const int64_t b0 = (int64_t)blockIdx.x * BK_CHUNK, b1 = min(n, b0 + BK_CHUNK);
+    for (int64_t i = b0 + threadIdx.x; i < b1; i += BK_THREADS) atomicAdd(&h[(uint32_t)(keys[i] >> shift)], 1u);
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < nbk; i += BK_THREADS)
+        if (h[i]) atomicAdd(&counts[i], h[i]);
+}
+
+// offs[0..nbk] exclusive prefix of counts; cursor[i] = 0
+__global__ __launch_bounds__(1024) void k_bucket_scan(const uint32_t* __restrict__ counts, uint32_t nbk,
+                                                      uint32_t* __restrict__ offs, uint32_t* __restrict__ cursor) {
+    __shared__ uint32_t part[1024];
+    const uint32_t per = (nbk + 1023) / 1024;
+    const uint32_t t = threadIdx.x, i0 = t * per;
+    uint32_t s = 0;
+    for (uint32_t i = i0; i < min(nbk, i0 + per); ++i) s += counts[i];
+    part[t] = s;
+    __syncthreads();
+    for (uint32_t o = 1; o < 1024; o <<= 1) {   // Hillis-Steele inclusive scan of the thread sums
+        const uint32_t v = t >= o ? part[t - o] : 0u;
+        __syncthreads();
+        part[t] += v;
+        __syncthreads();
+    }
+    uint32_t run = t ? part[t - 1] : 0u;
+    for (uint32_t i = i0; i < min(nbk, i0 + per); ++i) {
+        offs[i] = run;
+        run += counts[i];
+        cursor[i] = 0u;
+    }
+    if (t == 1023) offs[nbk] = part[1023];
+}
+
+__global__ __launch_bounds__(BK_THREADS) void k_bucket_scatter(const uint64_t* __restrict__ keys, int64_t n,
+                                                               int shift, uint32_t nbk,
+                                                               const uint32_t* __restrict__ offs,
+                                                               uint32_t* __restrict__ cursor,
+                                                               uint64_t* __restrict__ out) {
+    constexpr int PER = BK_CHUNK / BK_THREADS;
+    __shared__ uint32_t h[1 << BK_MAX_BITS];
+    __shared__ uint32_t base[1 << BK_MAX_BITS];
+    for (uint32_t i = threadIdx.x; i < nbk; i += BK_THREADS) h[i] = 0;
+    __syncthreads();
+    const int64_t b0 = (int64_t)blockIdx.x * BK_CHUNK;
+    uint64_t k[PER];
+    uint32_t rank[PER];
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+        const int64_t i = b0 + j * BK_THREADS + threadIdx.x;
+        k[j] = i < n ? keys[i] : 0ull;
+        rank[j] = i < n ? atomicAdd(&h[(uint32_t)(k[j] >> shift)], 1u) : 0u;   // order within a bucket: any
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < nbk; i += BK_THREADS)
+        base[i] = h[i] ? offs[i] + atomicAdd(&cursor[i], h[i]) : 0u;
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+        const int64_t i = b0 + j * BK_THREADS + threadIdx.x;
+        if (i < n) out[base[(uint32_t)(k[j] >> shift)] + rank[j]] = k[j];
+    }
+}
+
+// keys (n, packed: key bits [lo_bit, hi_bit), slot bits below) -> sorted by
+// the key bits into out (order among equal keys: any).  tmp: n u64;
+// small: 3 * 4096 + 1 u32; temp / temp_bytes: the caller's growable scratch.
+hipError_t bucket_sort_keys(const uint64_t* keys, uint64_t* tmp, uint64_t* out, int64_t n, int lo_bit, int hi_bit,
+                            uint32_t* small, void** temp, size_t* temp_bytes, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    if (n > 0xFFFFFFFFll || hi_bit > 64 || lo_bit < 0 || hi_bit <= lo_bit) return hipErrorInvalidValue;
+    int bb = 1;
+    while (bb < BK_MAX_BITS && (n >> (bb + 10)) > 0) ++bb;   // ~1 K keys per bucket
+    bb = std::min(bb, hi_bit - lo_bit);
+    const int shift = hi_bit - bb;
+    const uint32_t nbk = 1u << bb;
+    uint32_t* counts = small;
+    uint32_t* offs = small + (1 << BK_MAX_BITS);
+    uint32_t* cursor = small + 2 * (1 << BK_MAX_BITS) + 1;
+    hipError_t e = hipMemsetAsync(counts, 0, nbk * 4, s);
+    if (e != hipSuccess) return e;
+    const unsigned nwg = (unsigned)((n + BK_CHUNK - 1) / BK_CHUNK);
+    hipLaunchKernelGGL(k_bucket_hist, dim3(nwg), dim3(BK_THREADS), 0, s, keys, n, shift, nbk, counts);
+    hipLaunchKernelGGL(k_bucket_scan, dim3(1), dim3(1024), 0, s, counts, nbk, offs, cursor);
+    hipLaunchKernelGGL(k_bucket_scatter, dim3(nwg), dim3(BK_THREADS), 0, s, keys, n, shift, nbk, offs, cursor, tmp);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    if (shift <= lo_bit) {   // the buckets are the keys: already grouped and ordered
+        return hipMemcpyAsync(out, tmp, (size_t)n * 8, hipMemcpyDeviceToDevice, s);
+    }
+    size_t need = 0;
+    e = rocprim::segmented_radix_sort_keys(nullptr, need, tmp, out, (unsigned)n, nbk, offs, offs + 1,
+                                           (unsigned)lo_bit, (unsigned)shift, s);
+    if (e != hipSuccess) return e;
+    ensure(temp, *temp_bytes, need + 256);
+    size_t have = *temp_bytes;
+    return rocprim::segmented_radix_sort_keys(*temp, have, tmp, out, (unsigned)n, nbk, offs, offs + 1,
+                                              (unsigned)lo_bit, (unsigned)shift, s);
+}
+
+}  // namespace ctg

@@ -351,3 +351,33 @@ def test_graph_on_label_multiset_input(gpu, tmp_path):
             np.testing.assert_array_equal(g['nodes'].read_chunk(pos),
                                           np.unique(lab[tuple(slice(x, y) for x, y in zip(bb.begin, bb.end))]))
     np.testing.assert_array_equal(ndist.Graph(p, 'graph').uvIds(), O.rag_edges(lab))
+
+
+def test_number_of_nodes_literal_restatement(gpu, tmp_path):
+    """test_graph.py:108-113 literally: on dense labels 0..max the merged
+    graph's numberOfNodes equals gridRag's max + 1; per block (:79-81) the
+    rag's max + 1 is >= the block graph's numberOfNodes.  With gaps in the
+    labels numberOfNodes stays the distinct count."""
+    lab, _ = S.generate(SHAPE, cell=5, seed=33, with_boundary=False)
+    _, dense = np.unique(lab, return_inverse=True)
+    dense = dense.reshape(lab.shape).astype(np.uint64)          # labels 0..n-1, every one present
+    p = _setup(tmp_path, dense)
+    blk, ids = _graph(p, False)
+    full = ndist.Graph(p, 'graph')
+    assert full.numberOfNodes == int(dense.max()) + 1               # :110-113
+    with n5.File(p, 'r') as f:
+        g = f['s0/sub_graphs']
+        for b in ids:
+            bb = blk.getBlock(b)
+            edges = g['edges'].read_chunk(blk.blockGridPosition(b))
+            if edges is None:
+                continue
+            outer = tuple(slice(max(x - 1, 0), y) for x, y in zip(bb.begin, bb.end))
+            assert int(dense[outer].max()) + 1 >= ndist.Graph(edges.reshape(-1, 2)).numberOfNodes   # :79-81
+    gapped = dense * 3 + 5                                          # same RAG, labels with gaps
+    (tmp_path / 'gapped').mkdir()
+    p2 = _setup(tmp_path / 'gapped', gapped)
+    _graph(p2, False)
+    g2 = ndist.Graph(p2, 'graph')
+    assert g2.numberOfNodes == len(np.unique(gapped)) < int(gapped.max()) + 1
+    assert g2.numberOfEdges == full.numberOfEdges

@@ -487,3 +487,23 @@ def test_variance_constant_and_near_constant_edges(gpu):
     assert np.all(f[const, 1] == 0.0)
     np.testing.assert_allclose(f[~const, 1], f_ref[~const, 1], rtol=RTOL, atol=0)
     np.testing.assert_allclose(f[:, 0], f_ref[:, 0], rtol=1e-12, atol=0)
+
+
+def test_bucket_sort_skewed_keys(gpu, monkeypatch):
+    """The record sort's MSD bucket pass (ctg_sort.hip) on a skewed key set:
+    every third plane is background label 0, adjacent to nearly every cell, so
+    one bucket holds a large share of the records (the segmented sort's
+    large-segment path).  Same result as the plain radix sort and the oracle."""
+    lab, bnd = S.generate((48, 64, 80), cell=4, seed=9)
+    lab = lab.copy()
+    lab[::3] = 0
+    out = rag.rag_features(lab, bnd)
+    monkeypatch.setenv('CTG_BUCKET_SORT', '0')
+    ref = rag.rag_features(lab, bnd)
+    np.testing.assert_array_equal(out['edges'], ref['edges'])
+    np.testing.assert_array_equal(out['nodes'], ref['nodes'])
+    np.testing.assert_array_equal(out['features'][:, 9], ref['features'][:, 9])
+    np.testing.assert_allclose(out['features'], ref['features'], rtol=1e-12, atol=1e-15)
+    e_o, f_o = O.boundary_features(lab, bnd)
+    np.testing.assert_array_equal(out['edges'], e_o)
+    check_features(out['features'], f_o)
