@@ -28,6 +28,9 @@ hipError_t launch_pack_regions(const uint64_t* key, int64_t rcap, const RegionPr
 hipError_t launch_pack_pairs(int64_t n, const uint64_t* uv, int nb, uint64_t* sk, uint32_t* idx, hipStream_t s);
 hipError_t bucket_sort_keys(const uint64_t* keys, uint64_t* tmp, uint64_t* out, int64_t n, int lo_bit, int hi_bit,
                             uint32_t* small, void** temp, size_t* temp_bytes, hipStream_t s);
+hipError_t bucket_sort_pairs(const uint64_t* keys, const uint32_t* vals, uint64_t* ktmp, uint32_t* vtmp,
+                             uint64_t* kout, uint32_t* vout, int64_t n, int hi_bit, uint32_t* small, void** temp,
+                             size_t* temp_bytes, hipStream_t s);
 hipError_t launch_max_pairs(int64_t n, const uint64_t* uv, unsigned long long* out, hipStream_t s);
 hipError_t launch_reduce(int64_t E, const uint32_t* dE, const uint64_t* uniq, const uint32_t* runs,
                          const uint32_t* offs, const uint32_t* perm32, const uint64_t* perm64, int ib,
@@ -253,6 +256,14 @@ static bool bucket_sort() {
     const char* e = getenv("CTG_BUCKET_SORT");   // read per call: A/B and tests switch it
     return !(e && e[0] == '0');
 }
+// The pair path's bucket sort pays up to ~30 M records (1024^3 3-channel: 1.09 -> 1.00 ms at
+// 15.6 M; 2048^3: equal at 28 M) and loses on configs[4]'s 190 M (9.5 -> 12.8 ms: buckets of
+// ~46 K records go to the segmented sort's slower large-segment path); CTG_BUCKET_SORT_PAIRS=0/1 forces it.
+static bool bucket_sort_pairs_on(int64_t n) {
+    const char* e = getenv("CTG_BUCKET_SORT_PAIRS");
+    if (e) return e[0] == '1';
+    return n <= (int64_t)(32 << 20);
+}
 static int64_t sort_wide_digits_max() {
     static const int64_t v = [] {
         const char* e = getenv("CTG_SORT_WIDE_MAX");
@@ -355,6 +366,12 @@ static hipError_t reduce_records(Workspace& w, const ReduceJob& J, hipStream_t s
         ev.mark(3);
         auto key_only = rocprim::make_transform_iterator(w.sk_out, [ib] __device__(uint64_t k) { return k >> ib; });
         ROCPRIM_CALL(w, rocprim::run_length_encode(t, tbytes, key_only, (unsigned)n, w.uniq, w.runs, dE_all, s));
+    } else if (bucket_sort_pairs_on(n)) {
+        // tmp buffers: w.uniq (keys) and w.keep (values) are free until the
+        // run-length pass / the reduction
+        e = bucket_sort_pairs(w.sk_in, w.idx_in, w.uniq, w.keep, w.sk_out, w.idx_out, n, ub + nb, w.bsort, &w.temp,
+                              &w.temp_bytes, s);
+        if (e != hipSuccess) return e;
     } else if (n <= sort_wide_digits_max()) {
         ROCPRIM_CALL(w, rocprim::radix_sort_pairs<RecordSortConfig>(t, tbytes, w.sk_in, w.sk_out, w.idx_in,
                                                                     w.idx_out, (size_t)n, 0u, (unsigned)(ub + nb), s));

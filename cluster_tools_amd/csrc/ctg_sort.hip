@@ -94,6 +94,83 @@ __global__ __launch_bounds__(BK_THREADS) void k_bucket_scatter(const uint64_t* _
     }
 }
 
+// (key, value) pairs to their buckets (as k_bucket_scatter)
+__global__ __launch_bounds__(BK_THREADS) void k_bucket_scatter_pairs(const uint64_t* __restrict__ keys,
+                                                                     const uint32_t* __restrict__ vals, int64_t n,
+                                                                     int shift, uint32_t nbk,
+                                                                     const uint32_t* __restrict__ offs,
+                                                                     uint32_t* __restrict__ cursor,
+                                                                     uint64_t* __restrict__ kout,
+                                                                     uint32_t* __restrict__ vout) {
+    constexpr int PER = BK_CHUNK / BK_THREADS;
+    __shared__ uint32_t h[1 << BK_MAX_BITS];
+    __shared__ uint32_t base[1 << BK_MAX_BITS];
+    for (uint32_t i = threadIdx.x; i < nbk; i += BK_THREADS) h[i] = 0;
+    __syncthreads();
+    const int64_t b0 = (int64_t)blockIdx.x * BK_CHUNK;
+    uint64_t k[PER];
+    uint32_t rank[PER];
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+        const int64_t i = b0 + j * BK_THREADS + threadIdx.x;
+        k[j] = i < n ? keys[i] : 0ull;
+        rank[j] = i < n ? atomicAdd(&h[(uint32_t)(k[j] >> shift)], 1u) : 0u;
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < nbk; i += BK_THREADS)
+        base[i] = h[i] ? offs[i] + atomicAdd(&cursor[i], h[i]) : 0u;
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+        const int64_t i = b0 + j * BK_THREADS + threadIdx.x;
+        if (i < n) {
+            const uint32_t d = base[(uint32_t)(k[j] >> shift)] + rank[j];
+            kout[d] = k[j];
+            vout[d] = vals[i];
+        }
+    }
+}
+
+static int bucket_bits(int64_t n, int key_bits) {
+    int bb = 1;
+    while (bb < BK_MAX_BITS && (n >> (bb + 10)) > 0) ++bb;   // ~1 K keys per bucket
+    return std::min(bb, key_bits);
+}
+
+// (keys, vals) sorted by key bits [0, hi_bit) into (kout, vout); ktmp / vtmp: n each
+hipError_t bucket_sort_pairs(const uint64_t* keys, const uint32_t* vals, uint64_t* ktmp, uint32_t* vtmp,
+                             uint64_t* kout, uint32_t* vout, int64_t n, int hi_bit, uint32_t* small, void** temp,
+                             size_t* temp_bytes, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    if (n > 0xFFFFFFFFll || hi_bit > 64 || hi_bit <= 0) return hipErrorInvalidValue;
+    const int bb = bucket_bits(n, hi_bit);
+    const int shift = hi_bit - bb;
+    const uint32_t nbk = 1u << bb;
+    uint32_t* counts = small;
+    uint32_t* offs = small + (1 << BK_MAX_BITS);
+    uint32_t* cursor = small + 2 * (1 << BK_MAX_BITS) + 1;
+    hipError_t e = hipMemsetAsync(counts, 0, nbk * 4, s);
+    if (e != hipSuccess) return e;
+    const unsigned nwg = (unsigned)((n + BK_CHUNK - 1) / BK_CHUNK);
+    hipLaunchKernelGGL(k_bucket_hist, dim3(nwg), dim3(BK_THREADS), 0, s, keys, n, shift, nbk, counts);
+    hipLaunchKernelGGL(k_bucket_scan, dim3(1), dim3(1024), 0, s, counts, nbk, offs, cursor);
+    hipLaunchKernelGGL(k_bucket_scatter_pairs, dim3(nwg), dim3(BK_THREADS), 0, s, keys, vals, n, shift, nbk, offs,
+                       cursor, ktmp, vtmp);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    if (shift <= 0) {
+        e = hipMemcpyAsync(kout, ktmp, (size_t)n * 8, hipMemcpyDeviceToDevice, s);
+        return e != hipSuccess ? e : hipMemcpyAsync(vout, vtmp, (size_t)n * 4, hipMemcpyDeviceToDevice, s);
+    }
+    size_t need = 0;
+    e = rocprim::segmented_radix_sort_pairs(nullptr, need, ktmp, kout, vtmp, vout, (unsigned)n, nbk, offs, offs + 1,
+                                            0u, (unsigned)shift, s);
+    if (e != hipSuccess) return e;
+    ensure(temp, *temp_bytes, need + 256);
+    size_t have = *temp_bytes;
+    return rocprim::segmented_radix_sort_pairs(*temp, have, ktmp, kout, vtmp, vout, (unsigned)n, nbk, offs, offs + 1,
+                                               0u, (unsigned)shift, s);
+}
+
 // keys (n, packed: key bits [lo_bit, hi_bit), slot bits below) -> sorted by
 // the key bits into out (order among equal keys: any).  tmp: n u64;
 // small: 3 * 4096 + 1 u32; temp / temp_bytes: the caller's growable scratch.
@@ -101,9 +178,7 @@ hipError_t bucket_sort_keys(const uint64_t* keys, uint64_t* tmp, uint64_t* out, 
                             uint32_t* small, void** temp, size_t* temp_bytes, hipStream_t s) {
     if (n <= 0) return hipSuccess;
     if (n > 0xFFFFFFFFll || hi_bit > 64 || lo_bit < 0 || hi_bit <= lo_bit) return hipErrorInvalidValue;
-    int bb = 1;
-    while (bb < BK_MAX_BITS && (n >> (bb + 10)) > 0) ++bb;   // ~1 K keys per bucket
-    bb = std::min(bb, hi_bit - lo_bit);
+    const int bb = bucket_bits(n, hi_bit - lo_bit);
     const int shift = hi_bit - bb;
     const uint32_t nbk = 1u << bb;
     uint32_t* counts = small;
