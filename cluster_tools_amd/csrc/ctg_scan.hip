@@ -68,8 +68,12 @@ constexpr int STAGE_CAP = WAVE * NPER;                    // stage entries per w
 // folds at most this many samples between two table flushes (it requests a
 // flush before a batch would exceed it), so no entry can pass the bound.
 constexpr uint32_t WAVE_SAMPLE_BUDGET = 65535u / WAVES;
+// flush past 5/8 of the table: more live entries per flush interval, fewer
+// records (A/B over the BASELINE workloads, tools/ab_run.sh: 256 -> 320 cut
+// configs[4]'s records 191 M -> 148 M and its step 36.7 -> 32.2 ms, equal at
+// 512^3; 384+ lengthens the probe chains and slows the scan)
 #ifndef CTG_FILL_SOFT
-#define CTG_FILL_SOFT (TABLE_CAP / 2)
+#define CTG_FILL_SOFT (TABLE_CAP * 5 / 8)
 #endif
 constexpr uint32_t FILL_SOFT = CTG_FILL_SOFT;
 // poll the flush request after every fold batch (1) or only at plane ends (0)
