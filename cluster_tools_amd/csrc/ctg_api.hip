@@ -28,6 +28,8 @@ hipError_t launch_pack_regions(const uint64_t* key, int64_t rcap, const RegionPr
 hipError_t launch_pack_pairs(int64_t n, const uint64_t* uv, int nb, uint64_t* sk, uint32_t* idx, hipStream_t s);
 hipError_t bucket_sort_keys(const uint64_t* keys, uint64_t* tmp, uint64_t* out, int64_t n, int lo_bit, int hi_bit,
                             uint32_t* small, void** temp, size_t* temp_bytes, hipStream_t s);
+hipError_t bucket_runs(const uint64_t* sorted, int64_t n, int lo_bit, int hi_bit, uint32_t* small, uint64_t* uniq,
+                       uint32_t* runs, uint32_t* roffs, uint32_t* dE, hipStream_t s);
 hipError_t bucket_sort_pairs(const uint64_t* keys, const uint32_t* vals, uint64_t* ktmp, uint32_t* vtmp,
                              uint64_t* kout, uint32_t* vout, int64_t n, int hi_bit, uint32_t* small, void** temp,
                              size_t* temp_bytes, hipStream_t s);
@@ -166,7 +168,7 @@ static hipError_t ws_init(Workspace& w) {
     if (e != hipSuccess) return e;
     e = hipMalloc(&w.small, 64 * sizeof(unsigned int));
     if (e != hipSuccess) return e;
-    e = hipMalloc(&w.bsort, (3 * 4096 + 1) * sizeof(uint32_t));   // bucket sort counts / offsets / cursors
+    e = hipMalloc(&w.bsort, BK_SMALL_WORDS * sizeof(uint32_t));   // bucket sort scratch
     if (e != hipSuccess) return e;
     e = hipHostMalloc(&w.small_host, 64 * sizeof(unsigned int), hipHostMallocDefault);
     if (e != hipSuccess) return e;
@@ -352,14 +354,17 @@ static hipError_t reduce_records(Workspace& w, const ReduceJob& J, hipStream_t s
     else e = launch_pack_pairs(n, J.pairs, nb, w.sk_in, w.idx_in, s);
     if (e != hipSuccess) return e;
     ev.mark(2);
+    bool have_offs = false;   // run offsets already written (bucket path)
     if (packed && bucket_sort()) {
         // MSD bucket pass + segmented sort of the key bits (ctg_sort.hip):
         // 4 fused launches instead of 4 onesweep passes with their fills
         e = bucket_sort_keys(w.sk_in, w.uniq, w.sk_out, n, ib, ib + ub + nb, w.bsort, &w.temp, &w.temp_bytes, s);
         if (e != hipSuccess) return e;
         ev.mark(3);
-        auto key_only = rocprim::make_transform_iterator(w.sk_out, [ib] __device__(uint64_t k) { return k >> ib; });
-        ROCPRIM_CALL(w, rocprim::run_length_encode(t, tbytes, key_only, (unsigned)n, w.uniq, w.runs, dE_all, s));
+        // runs from the buckets: unique keys, lengths and offsets in one go
+        e = bucket_runs(w.sk_out, n, ib, ib + ub + nb, w.bsort, w.uniq, w.runs, w.offs, dE_all, s);
+        if (e != hipSuccess) return e;
+        have_offs = true;
     } else if (packed) {
         ROCPRIM_CALL(w, rocprim::radix_sort_keys<RecordSortConfig>(t, tbytes, w.sk_in, w.sk_out, (size_t)n,
                                                                    (unsigned)ib, (unsigned)(ib + ub + nb), s));
@@ -384,7 +389,9 @@ static hipError_t reduce_records(Workspace& w, const ReduceJob& J, hipStream_t s
         ROCPRIM_CALL(w, rocprim::run_length_encode(t, tbytes, w.sk_out, (unsigned)n, w.uniq, w.runs, dE_all, s));
     }
     // offsets over the n-bound: entries past E_all are never read
-    ROCPRIM_CALL(w, rocprim::exclusive_scan(t, tbytes, w.runs, w.offs, 0u, (size_t)n, rocprim::plus<uint32_t>(), s));
+    if (!have_offs)
+        ROCPRIM_CALL(w, rocprim::exclusive_scan(t, tbytes, w.runs, w.offs, 0u, (size_t)n, rocprim::plus<uint32_t>(),
+                                                s));
     ev.mark(4);
 
     // outputs (uncompacted), sized by the bound n
@@ -449,6 +456,8 @@ static hipError_t reduce_records(Workspace& w, const ReduceJob& J, hipStream_t s
         e = launch_mark_nodes(n, dE_all, w.uniq, nb, bits, s);
         if (e != hipSuccess) return e;
         // word offsets = exclusive scan of the words' popcounts (read through the scan's input iterator)
+        // (tried: the scan and the expansion in one workgroup for small label ranges -- 0.053 -> 0.115 ms
+        // at 512^3, the serial per-thread expansion loses to the wide launch)
         auto popc = rocprim::make_transform_iterator(bits, [] __device__(uint32_t b) { return (uint32_t)__popc(b); });
         ROCPRIM_CALL(w, rocprim::exclusive_scan(t, tbytes, popc, off, 0u, (size_t)W, rocprim::plus<uint32_t>(), s));
         e = launch_bits_to_nodes(W, bits, off, res->nodes, dN, s);

@@ -176,6 +176,8 @@ struct ReduceOut {
     int ablate;           // diagnostics (CTG_REDUCE_ABLATE): 1 no quantiles, 2 no record loads, 4 no feature stores
 };
 
+constexpr int BK_SMALL_WORDS = 5 * 4096 + 16;   // bucket sort: counts, offsets, cursors, run heads
+
 struct Workspace {
     int device = -1;
     RecordBuf rec;
@@ -191,7 +193,7 @@ struct Workspace {
     Counters* counters_host = nullptr;   // pinned
     unsigned int* small = nullptr;       // device scalars (run counts etc.)
     unsigned int* small_host = nullptr;
-    uint32_t* bsort = nullptr;           // device: bucket-sort counts / offsets / cursors (ctg_sort.hip)
+    uint32_t* bsort = nullptr;           // device: bucket-sort scratch, BK_SMALL_WORDS u32 (ctg_sort.hip)
     // host->device staging of volumes
     void* stage[2] = {nullptr, nullptr};
     size_t stage_bytes[2] = {0, 0};

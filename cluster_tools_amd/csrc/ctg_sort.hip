@@ -26,6 +26,7 @@ namespace ctg {
 constexpr int BK_THREADS = 256;
 constexpr int BK_CHUNK = 4096;   // keys per workgroup in the histogram / scatter
 constexpr int BK_MAX_BITS = 12;  // at most 4096 buckets (LDS counters)
+static_assert(5 * (1 << BK_MAX_BITS) + 2 <= BK_SMALL_WORDS, "bucket-sort scratch (ctg_internal.h)");
 
 __global__ __launch_bounds__(BK_THREADS) void k_bucket_hist(const uint64_t* __restrict__ keys, int64_t n, int shift,
                                                             uint32_t nbk, uint32_t* __restrict__ counts) {
@@ -169,6 +170,92 @@ hipError_t bucket_sort_pairs(const uint64_t* keys, const uint32_t* vals, uint64_
     size_t have = *temp_bytes;
     return rocprim::segmented_radix_sort_pairs(*temp, have, ktmp, kout, vtmp, vout, (unsigned)n, nbk, offs, offs + 1,
                                                0u, (unsigned)shift, s);
+}
+
+// ---------------------------------------------------------------------------
+// Runs of equal keys after bucket_sort_keys (the back half's "segment" step):
+// runs never cross buckets, so heads are counted per bucket (one workgroup
+// each), the bucket counts scanned (k_bucket_scan), and every bucket writes
+// its unique keys, run offsets and run lengths at its base -- three light
+// launches instead of rocPRIM's run-length encode and exclusive scan.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ bool is_head(const uint64_t* k, uint32_t i, uint32_t b0, int ib) {
+    return i == b0 || (k[i] >> ib) != (k[i - 1] >> ib);
+}
+
+__global__ __launch_bounds__(BK_THREADS) void k_run_heads_count(const uint64_t* __restrict__ keys, int ib,
+                                                                const uint32_t* __restrict__ offs,
+                                                                uint32_t* __restrict__ hc) {
+    __shared__ uint32_t red[BK_THREADS / 64];
+    const uint32_t b = blockIdx.x, b0 = offs[b], b1 = offs[b + 1];
+    uint32_t c = 0;
+    for (uint32_t i = b0 + threadIdx.x; i < b1; i += BK_THREADS) c += is_head(keys, i, b0, ib) ? 1u : 0u;
+    for (int o = 32; o > 0; o >>= 1) c += (uint32_t)__shfl_xor((int)c, o, 64);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t t = 0;
+        for (int w = 0; w < BK_THREADS / 64; ++w) t += red[w];
+        hc[b] = t;
+    }
+}
+
+__global__ __launch_bounds__(BK_THREADS) void k_run_heads_write(const uint64_t* __restrict__ keys, int ib,
+                                                                uint32_t nbk, const uint32_t* __restrict__ offs,
+                                                                const uint32_t* __restrict__ ho,
+                                                                uint64_t* __restrict__ uniq, uint32_t* __restrict__ runs,
+                                                                uint32_t* __restrict__ roffs, uint32_t* __restrict__ dE) {
+    __shared__ uint32_t wsum[BK_THREADS / 64];
+    const uint32_t b = blockIdx.x, b0 = offs[b], b1 = offs[b + 1];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    if (b == 0 && threadIdx.x == 0) *dE = ho[nbk];
+    uint32_t base = ho[b];
+    for (uint32_t c0 = b0; c0 < b1; c0 += BK_THREADS) {
+        const uint32_t i = c0 + threadIdx.x;
+        const bool h = i < b1 && is_head(keys, i, b0, ib);
+        const uint64_t m = __ballot(h);
+        const uint32_t r = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+        if (lane == 0) wsum[wv] = (uint32_t)__popcll(m);
+        __syncthreads();
+        uint32_t before = 0, total = 0;
+#pragma unroll
+        for (int w = 0; w < BK_THREADS / 64; ++w) {
+            before += w < wv ? wsum[w] : 0u;
+            total += wsum[w];
+        }
+        if (h) {
+            const uint32_t e = base + before + r;
+            const uint64_t k = keys[i] >> ib;
+            uint32_t j = i + 1;
+            while (j < b1 && (keys[j] >> ib) == k) ++j;   // runs are short (~2 records per edge)
+            uniq[e] = k;
+            roffs[e] = i;
+            runs[e] = j - i;
+        }
+        base += total;
+        __syncthreads();
+    }
+}
+
+// (sorted keys of bucket_sort_keys with the same n / lo_bit / hi_bit) ->
+// uniq keys (>> lo_bit), run lengths, run offsets, *dE = number of runs
+hipError_t bucket_runs(const uint64_t* sorted, int64_t n, int lo_bit, int hi_bit, uint32_t* small, uint64_t* uniq,
+                       uint32_t* runs, uint32_t* roffs, uint32_t* dE, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    const int bb = bucket_bits(n, hi_bit - lo_bit);
+    const uint32_t nbk = 1u << bb;
+    // small layout (BK_SMALL_WORDS): counts [0, M), bucket offsets [M, 2M+1),
+    // cursors [2M+1, 3M+1) -- free now, they hold the head counts --, head
+    // offsets [3M+1, 4M+2), scratch for the scan's cursor output [4M+2, 5M+2)
+    constexpr uint32_t M = 1u << BK_MAX_BITS;
+    const uint32_t* offs = small + M;
+    uint32_t* hc = small + 2 * M + 1;
+    uint32_t* ho = small + 3 * M + 1;
+    hipLaunchKernelGGL(k_run_heads_count, dim3(nbk), dim3(BK_THREADS), 0, s, sorted, lo_bit, offs, hc);
+    hipLaunchKernelGGL(k_bucket_scan, dim3(1), dim3(1024), 0, s, hc, nbk, ho, small + 4 * M + 2);
+    hipLaunchKernelGGL(k_run_heads_write, dim3(nbk), dim3(BK_THREADS), 0, s, sorted, lo_bit, nbk, offs, ho, uniq,
+                       runs, roffs, dE);
+    return hipGetLastError();
 }
 
 // keys (n, packed: key bits [lo_bit, hi_bit), slot bits below) -> sorted by
