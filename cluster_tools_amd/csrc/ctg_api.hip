@@ -789,13 +789,15 @@ int ctg_rag_features(const void* labels, int label_bits, const void* data, int d
     // depend on it: ctg_scan.hip's per-wave sample budget bounds every count)
     P.check_planes = 8;
     if (const char* cp = getenv("CTG_CHECK_PLANES")) P.check_planes = std::max(1, atoi(cp));
-    // planes per workgroup: 32, fewer where that leaves < ~1024 workgroups
-    // (A/B with the 5/8 table fill: 32 planes vs 64 -- 512^3 step 1.027 -> 1.014 ms,
-    // configs[4] 32.2 -> 30.0 ms with records 148 M -> 134 M, 2048^3 within 0.3 %)
+    // planes per workgroup: 32, fewer where that leaves < ~1024 workgroups,
+    // 64 where even 64-plane tiles give >= 32 K workgroups (A/B with the 5/8
+    // table fill, 32 vs 64 planes: 512^3 step 1.027 -> 1.014 ms, configs[4]
+    // 32.2 -> 30.0 ms with records 148 M -> 134 M; 2048^3 scan 30.4 vs 30.9 ms
+    // favours 64)
     {
         const int64_t rows = scan_tile_rows();
         const int64_t cols = ((shape[2] + TILE_X - 1) / TILE_X) * ((shape[1] + rows - 1) / rows);
-        int tz = 32;
+        int tz = cols * ((shape[0] + 63) / 64) >= 32768 ? 64 : 32;
         while (tz > 8 && cols * ((shape[0] + tz - 1) / tz) < 1024) tz /= 2;
         if (const char* t = getenv("CTG_TILE_Z")) tz = std::max(1, atoi(t));
         P.tile_z = tz;
