@@ -173,6 +173,37 @@ def exchange(rows, send_counts, group=None, recv_counts=None):
     return out.to(dev)
 
 
+def exchange_rows_nodes(rows, e_send, e_recv, nodes, n_send, n_recv, group=None):
+    """One all_to_all for the edge rows (ROW_WORDS int64 each) and the node
+    ids: destination d gets [its rows, its node ids] as one int64 segment
+    (counts from the count matrix, known on every rank) -- one collective
+    instead of two per step."""
+    world = dist.get_world_size(group)
+    dev = rows.device
+    wire = _wire_device(dev, group)
+    rows = rows.reshape(-1, ROW_WORDS)
+    nodes = nodes.reshape(-1).to(torch.int64)
+    parts, r0, n0 = [], 0, 0
+    for d in range(world):
+        parts.append(rows[r0:r0 + int(e_send[d])].reshape(-1))
+        parts.append(nodes[n0:n0 + int(n_send[d])])
+        r0 += int(e_send[d])
+        n0 += int(n_send[d])
+    buf = torch.cat(parts).to(wire)
+    in_split = [int(e_send[d]) * ROW_WORDS + int(n_send[d]) for d in range(world)]
+    out_split = [int(e_recv[d]) * ROW_WORDS + int(n_recv[d]) for d in range(world)]
+    out = torch.empty(sum(out_split), dtype=torch.int64, device=wire)
+    dist.all_to_all_single(out, buf, output_split_sizes=out_split, input_split_sizes=in_split, group=group)
+    out = out.to(dev)
+    rr, nr, o = [], [], 0
+    for d in range(world):
+        rr.append(out[o:o + int(e_recv[d]) * ROW_WORDS])
+        o += int(e_recv[d]) * ROW_WORDS
+        nr.append(out[o:o + int(n_recv[d])])
+        o += int(n_recv[d])
+    return torch.cat(rr).reshape(-1, ROW_WORDS), torch.cat(nr)
+
+
 def all_gather_tensor(t, group=None):
     """all_gather of equal-shape tensors -> list (on t's device)."""
     wire = _wire_device(t.device, group)
@@ -286,8 +317,8 @@ def rag_features_distributed(labels, data=None, offsets=None, own_begin=None, ow
 
     Collectives: one all_gather of the splitter samples, one all_gather of
     the (edge, node) send-count matrix -- the only host round trip before the
-    data moves --, one all_to_all of edge rows, one of node ids, and the
-    all_gather of the shard sizes.  Splitters and counts are computed on the
+    data moves --, one all_to_all of the edge rows and node ids together, and
+    the all_gather of the shard sizes.  Splitters and counts are computed on the
     wire device, so with RCCL nothing but the count matrix leaves HBM.
     """
     shape = tuple(labels.shape)
@@ -335,7 +366,7 @@ def rag_features_distributed(labels, data=None, offsets=None, own_begin=None, ow
     if not packable:
         # general labels: every row goes to the owner of its u and is merged there
         rows = pack_rows(keys, sums, recs)
-        recv = exchange(rows, e_send, group, recv_counts=e_recv_all)
+        recv, nrecv = exchange_rows_nodes(rows, e_send, e_recv_all, nodes, n_send, n_recv, group)
         rk, rs, rr = unpack_rows(recv)
         me, mf = backend.merge(rk, rs, rr, hist_range)
         merged = {'edges': me, 'features': mf}
@@ -349,7 +380,7 @@ def rag_features_distributed(labels, data=None, offsets=None, own_begin=None, ow
         recv_counts[rank] = 0
         out_k = torch.cat([keys[:lo_i], keys[hi_i:]])
         out_rows = pack_rows(out_k, torch.cat([sums[:lo_i], sums[hi_i:]]), torch.cat([recs[:lo_i], recs[hi_i:]]))
-        recv = exchange(out_rows, send, group, recv_counts=recv_counts)
+        recv, nrecv = exchange_rows_nodes(out_rows, send, recv_counts, nodes, n_send, n_recv, group)
         lk, ls, lr, lf = keys[lo_i:hi_i], sums[lo_i:hi_i], recs[lo_i:hi_i], feats[lo_i:hi_i]
         if recv.shape[0] == 0:
             shared = torch.zeros(lk.shape[0], dtype=torch.bool, device=dev)
@@ -371,8 +402,7 @@ def rag_features_distributed(labels, data=None, offsets=None, own_begin=None, ow
             merged = _merge_sorted(lk[keep], lf[keep], me, mf)
     n_loc = int(merged['edges'].shape[0])
 
-    # nodes -> the same ranges (send counts known from the count matrix)
-    nrecv = exchange(nodes, n_send, group, recv_counts=n_recv)
+    # nodes went to the same ranges in the rows' all_to_all
     node_shard = backend.unique(nrecv)
 
     (e_off, e_tot), (n_off, n_tot) = _exclusive_offsets([n_loc, int(node_shard.shape[0])], group, dev)
