@@ -665,6 +665,57 @@ def accumulateInput(graph, input, labels, ignoreLabel, withSize, minVal, maxVal)
     return out
 
 
+# mergeFeatureBlocks jobs of one workflow each read every block's edge_ids and
+# feature chunks (merge_edge_features.py:127-147: the job's edge range is
+# selected after reading).  Job threads that run at the same time share one
+# decode: an entry lives only while a call that asked for it is still reading
+# (a later call reads the files again), and its key carries every chunk file's
+# (mtime, size).
+_merge_cache = {}
+_merge_cache_lock = threading.Lock()
+
+
+def _chunk_stamp(ds, positions):
+    out = []
+    for pos in positions:
+        try:
+            st = os.stat(ds._chunk_path(pos))
+            out.append((st.st_mtime_ns, st.st_size))
+        except OSError:
+            out.append(None)
+    return tuple(out)
+
+
+def _read_blocks_shared(ds_ids, ds_feat, positions, n_threads):
+    pos_key = tuple(tuple(int(x) for x in p) for p in positions)
+    key = (ds_ids.path, ds_feat.path, pos_key, _chunk_stamp(ds_ids, positions), _chunk_stamp(ds_feat, positions))
+    with _merge_cache_lock:
+        ent = _merge_cache.get(key)
+        owner = ent is None
+        if owner:
+            ent = {'ev': threading.Event(), 'val': None, 'err': None, 'users': 0}
+            _merge_cache[key] = ent
+        ent['users'] += 1
+    try:
+        if owner:
+            try:
+                ent['val'] = (ds_ids.read_chunks(positions, n_threads), ds_feat.read_chunks(positions, n_threads))
+            except Exception as e:   # every waiter re-raises
+                ent['err'] = e
+            finally:
+                ent['ev'].set()
+        else:
+            ent['ev'].wait()
+        if ent['err'] is not None:
+            raise ent['err']
+        return ent['val']
+    finally:
+        with _merge_cache_lock:
+            ent['users'] -= 1
+            if ent['users'] == 0 and _merge_cache.get(key) is ent:
+                del _merge_cache[key]
+
+
 def mergeFeatureBlocks(graphPath, subgraphKey, featuresPath, featuresKey, outPath, outKey,  # noqa: N802,N803
                        blockIds, edgeIdBegin, edgeIdEnd, numberOfThreads=1):  # noqa: N803
     """Combine the per-block feature rows of edges in [edgeIdBegin, edgeIdEnd)
@@ -682,6 +733,7 @@ def mergeFeatureBlocks(graphPath, subgraphKey, featuresPath, featuresKey, outPat
     non-empty rows, and count-weighted quantiles (nifty-compatible; the exact
     merged quantiles need the histograms)."""
     begin, end = int(edgeIdBegin), int(edgeIdEnd)
+    t = time.perf_counter()
     with _open(graphPath, 'r') as fg, _open(featuresPath, 'r') as ff:
         g = fg[subgraphKey]
         blk, _ = _subgraph_blocking(g)
@@ -693,8 +745,7 @@ def mergeFeatureBlocks(graphPath, subgraphKey, featuresPath, featuresKey, outPat
 
         block_ids = [int(b) for b in blockIds]
         positions = [blk.blockGridPosition(b) for b in block_ids]
-        all_ids = ds_ids.read_chunks(positions, numberOfThreads)
-        all_rows = ds_feat.read_chunks(positions, numberOfThreads)
+        all_ids, all_rows = _read_blocks_shared(ds_ids, ds_feat, positions, numberOfThreads)
         parts = []
         for b, ids, rows in zip(block_ids, all_ids, all_rows):
             if ids is None or rows is None:
@@ -706,6 +757,7 @@ def mergeFeatureBlocks(graphPath, subgraphKey, featuresPath, featuresKey, outPat
             sel = (ids >= begin) & (ids < end)
             if sel.any():
                 parts.append((ids[sel], rows[sel]))
+    t = _prof('merge_read', t)
     out = np.zeros((end - begin, N_FEATURES if have_stats else n_features), np.float64)
     if parts:
         ids = np.concatenate([p[0] for p in parts]).astype(np.uint64)
@@ -731,5 +783,7 @@ def mergeFeatureBlocks(graphPath, subgraphKey, featuresPath, featuresKey, outPat
                 m = rag.merge_feature_rows(ids, np.concatenate([rows[:, cols], size], axis=1), begin, end)
                 out[:, cols] = m[:, :N_FEATURES - 1]
                 out[:, -1] = m[:, -1]
+    t = _prof('merge_compute', t)
     with _open(outPath) as fo:
         fo[outKey][begin:end, :] = out
+    _prof('merge_write', t)
