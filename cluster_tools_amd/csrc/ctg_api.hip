@@ -355,7 +355,11 @@ static hipError_t reduce_records(Workspace& w, const ReduceJob& J, hipStream_t s
     if (e != hipSuccess) return e;
     ev.mark(2);
     bool have_offs = false;   // run offsets already written (bucket path)
-    if (packed && bucket_sort()) {
+    // the bucket pass needs keys spread over their top bits: block-tagged keys
+    // (ctg_rag_blocks, J.ub set) put the block id there and fill a few huge
+    // buckets (configs[0] device time 3.9 -> 6.7 ms), so they keep onesweep
+    const bool spread = J.ub == 0;
+    if (packed && spread && bucket_sort()) {
         // MSD bucket pass + segmented sort of the key bits (ctg_sort.hip):
         // 4 fused launches instead of 4 onesweep passes with their fills
         e = bucket_sort_keys(w.sk_in, w.uniq, w.sk_out, n, ib, ib + ub + nb, w.bsort, &w.temp, &w.temp_bytes, s);
@@ -371,7 +375,7 @@ static hipError_t reduce_records(Workspace& w, const ReduceJob& J, hipStream_t s
         ev.mark(3);
         auto key_only = rocprim::make_transform_iterator(w.sk_out, [ib] __device__(uint64_t k) { return k >> ib; });
         ROCPRIM_CALL(w, rocprim::run_length_encode(t, tbytes, key_only, (unsigned)n, w.uniq, w.runs, dE_all, s));
-    } else if (bucket_sort_pairs_on(n)) {
+    } else if (spread && bucket_sort_pairs_on(n)) {
         // tmp buffers: w.uniq (keys) and w.keep (values) are free until the
         // run-length pass / the reduction
         e = bucket_sort_pairs(w.sk_in, w.idx_in, w.uniq, w.keep, w.sk_out, w.idx_out, n, ub + nb, w.bsort, &w.temp,
