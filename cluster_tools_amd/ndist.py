@@ -425,11 +425,18 @@ class Graph:
 # features
 # ---------------------------------------------------------------------------
 
+# the statistics companion is the library's own intermediate (written by the
+# block jobs, read once by the merge jobs): uncompressed by default -- gzip,
+# even at level 1, made its write the slowest part of the per-block feature
+# stage (0.2 s of 0.62 s on configs[0]) and its decode the bulk of the merge
+# read; CTG_STATS_COMPRESSION=gzip trades that time for ~3x less disk
+STATS_COMPRESSION = os.environ.get('CTG_STATS_COMPRESSION', 'raw')
+
+
 def _stats_dataset(fo, outKey, shape, chunks):  # noqa: N803
-    # the library's own companion format: gzip level 1 (4-5x faster to write
-    # than z5's default level 5, which the reference-layout datasets keep)
+    comp = {'type': 'gzip', 'level': 1, 'useZlib': False} if STATS_COMPRESSION == 'gzip' else 'raw'
     return fo.require_dataset(outKey + STATS_SUFFIX, shape=shape, chunks=chunks, dtype='uint32',
-                              compression={'type': 'gzip', 'level': 1, 'useZlib': False})
+                              compression=comp)
 
 
 def encode_stats_words(sums, records):
@@ -506,6 +513,7 @@ def _block_features(graphPath, subgraphKey, dataPath, dataKey, labelsPath, label
     max_vox = max(sum(vox[i] for i in bt) for bt in batches)
     arenas = [(rag.host_arena(max_vox * 8), rag.host_arena(max_vox * max(1, n_ch) * data_dtype.itemsize))
               for _ in range(min(2, len(batches)))]
+    _prof('setup', t)
     try:
         _block_batches(batches, arenas, geo, vox, n_ch, data_dtype, dataPath, dataKey, labelsPath, labelsKey,
                        outPath, outKey, shape, chunks, offsets, ignore)
@@ -525,6 +533,7 @@ def _block_batches(batches, arenas, geo, vox, n_ch, data_dtype, dataPath, dataKe
 
         def load(k):
             """decode batch k into arena k % 2 -> (label arena, data arena, descriptors)"""
+            t0 = time.perf_counter()
             la, da = arenas[k % 2]
             descs, reads, lo_, do_ = [], [], 0, 0
             for i in batches[k]:
@@ -543,9 +552,11 @@ def _block_batches(batches, arenas, geo, vox, n_ch, data_dtype, dataPath, dataKe
                 do_ += v * max(1, n_ch)
             # every ROI of the batch decoded at once (each over its chunks)
             list(io.map(lambda r: _read_into(r[0], r[1], r[2], 2), reads))
+            _prof('load_thread', t0)
             return la.view(np.uint64, lo_), da.view(data_dtype, do_), descs
 
         def write(k, results):
+            t0 = time.perf_counter()
             pos, feats, words = [], [], []
             for i, res in zip(batches[k], results):
                 x = geo[i]
@@ -566,8 +577,11 @@ def _block_batches(batches, arenas, geo, vox, n_ch, data_dtype, dataPath, dataKe
                 pos.append(x['pos'])
                 feats.append(f.ravel())
                 words.append(encode_stats_words(sm, rc).ravel())
+            t0 = _prof('write_encode_thread', t0)
             ds_out.write_chunks(pos, feats, varlen=True)
+            t0 = _prof('write_features_thread', t0)
             ds_st.write_chunks(pos, words, varlen=True)
+            _prof('write_stats_thread', t0)
 
         with ThreadPoolExecutor(1) as reader, ThreadPoolExecutor(1) as writer, \
                 ThreadPoolExecutor(max(1, IO_THREADS // 2)) as io:
@@ -585,6 +599,7 @@ def _block_batches(batches, arenas, geo, vox, n_ch, data_dtype, dataPath, dataKe
                 t = _prof('compute', t)
                 if pending is not None:
                     pending.result()
+                    _prof('write_wait', t)
                 pending = writer.submit(write, k, results)
             if pending is not None:
                 t = time.perf_counter()
