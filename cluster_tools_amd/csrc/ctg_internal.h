@@ -31,7 +31,15 @@ constexpr int NREC_WORDS = 24;         // narrow record: 21 hist words + cnt + m
 //   words 0..3 (sum f64, sum of squares f64), 4..27 the NREC_WORDS, 28..31 zero
 constexpr int NREC_STRIDE = 32;
 constexpr int NREC_OFF = 4;
-constexpr int WREC_WORDS = 48;         // wide record: 42 u32 slots + cnt + min + max + pad
+constexpr int NREC_PIV = 28;           // word 28: the pivot (f32 bits) the two sums are taken about
+constexpr int WREC_WORDS = 48;         // wide record: 42 u32 slots + cnt + min + max + pivot + pad
+constexpr int WREC_PIV = 45;
+// Statistics are kept as shifted sums about a per-entry pivot p (the entry's
+// first sample): S1 = sum(x - p), S2 = sum((x - p)^2).  The variance
+// (S2 - S1^2/n)/n then cancels only the spread of the samples, not their
+// magnitude, and records / partial tables combine by re-pivoting
+// (Moments::add, ctg_reduce.hip).  A pivot word of 0 is the plain power sums.
+constexpr uint32_t PIV_EMPTY = 0xFFFFFFFFu;   // table entry without a pivot yet (a NaN no sample carries)
 constexpr uint32_t ADJ_FLAG = 0x80000000u;  // record/edge came from a nearest-neighbour face
 constexpr uint64_t EMPTY_KEY = ~0ull;
 constexpr int N_FEATURES = 10;

@@ -204,30 +204,53 @@ __host__ __device__ __forceinline__ void vigra_quantiles_cross(const HL& hl, dou
     }
 }
 
+// Shifted sums of one edge about the pivot p0 of its first non-empty record:
+// a record (n, S1, S2 about its own pivot p) is re-pivoted by d = p - p0,
+//   sum(x - p0) = S1 + n d,   sum((x - p0)^2) = S2 + d (2 S1 + n d),
+// where every term is bounded by the edge's sample spread (both pivots are
+// samples of the edge), so the variance keeps its relative accuracy however
+// large the samples are against their spread (Chan et al.'s pairwise update,
+// in sums form).
+// Branch-free: until a record with samples arrives (records without samples
+// carry zero sums), p0 follows the latest pivot, so d = 0 for the first one.
+struct Moments {
+    uint32_t n = 0;
+    double p0 = 0.0, S1 = 0.0, S2 = 0.0;
+    __device__ __forceinline__ void add(uint32_t ni, double s1, double s2, uint32_t pbits) {
+        const double p = (double)__uint_as_float(pbits);
+        p0 = n == 0 ? p : p0;
+        const double d = p - p0, nd = (double)ni * d;
+        S1 += s1 + nd;
+        S2 += s2 + d * (2.0 * s1 + nd);
+        n += ni;
+    }
+};
+
 template <bool WIDE>
 __device__ __forceinline__ void load_record(const RecordBuf& R, uint32_t i, uint32_t (&h)[NSLOTS], uint32_t& cnt,
-                                            uint32_t& flags, uint32_t& mn, uint32_t& mx, double& sum, double& sq) {
+                                            uint32_t& flags, uint32_t& mn, uint32_t& mx, Moments& mo) {
     if constexpr (!WIDE) {
-        // one 128-byte body: (sum, sumsq), then the 24 record words
+        // one 128-byte body: (S1, S2), the 24 record words, the pivot
         const uint4* p = (const uint4*)(R.hist + (size_t)i * NREC_STRIDE);
         const double2 sw = *reinterpret_cast<const double2*>(p);
-        sum += sw.x;
-        sq += sw.y;
         uint32_t w[NREC_WORDS];
 #pragma unroll
         for (int j = 0; j < NREC_WORDS / 4; ++j) {
             uint4 v = p[1 + j];
             w[4 * j] = v.x; w[4 * j + 1] = v.y; w[4 * j + 2] = v.z; w[4 * j + 3] = v.w;
         }
+        const uint32_t piv = p[7].x;
 #pragma unroll
         for (int j = 0; j < HWORDS; ++j) {
             h[2 * j] += w[j] & 0xFFFFu;
             h[2 * j + 1] += w[j] >> 16;
         }
-        cnt += w[21] & ~ADJ_FLAG;
+        const uint32_t n = w[21] & ~ADJ_FLAG;
+        cnt += n;
         flags |= w[21] & ADJ_FLAG;
         mn = min(mn, w[22]);
         mx = max(mx, w[23]);
+        mo.add(n, sw.x, sw.y, piv);
     } else {
         const uint4* p = (const uint4*)(R.hist + (size_t)i * WREC_WORDS);
         uint32_t w[WREC_WORDS];
@@ -238,13 +261,13 @@ __device__ __forceinline__ void load_record(const RecordBuf& R, uint32_t i, uint
         }
 #pragma unroll
         for (int j = 0; j < NSLOTS; ++j) h[j] += w[j];
-        cnt += w[42] & ~ADJ_FLAG;
+        const uint32_t n = w[42] & ~ADJ_FLAG;
+        cnt += n;
         flags |= w[42] & ADJ_FLAG;
         mn = min(mn, w[43]);
         mx = max(mx, w[44]);
         const double2 s2 = R.sums[i];
-        sum += s2.x;
-        sq += s2.y;
+        mo.add(n, s2.x, s2.y, w[WREC_PIV]);
     }
 }
 
@@ -292,19 +315,20 @@ __global__ __launch_bounds__(256) void k_reduce_edges(int64_t E, const uint32_t*
 #pragma unroll
         for (int j = 0; j < NSLOTS; ++j) h[j] = 0;
         uint32_t cnt = 0, mn = ORD_POS_INF, mx = ORD_NEG_INF;
-        double sum = 0.0, sq = 0.0;
+        Moments mo;
         const uint32_t b = offs[e], n = runs[e];
         if (O.ablate & 2) {
             cnt = n;
             h[1] = n;
             mn = mx = 0x3F800000u ^ 0x80000000u;
-            sum = sq = (double)n;
+            mo.add(n, 0.0, 0.0, 0u);
         } else {
             for (uint32_t r = b; r < b + n; ++r) {
                 const uint32_t i = perm(r);
-                load_record<WIDE>(R, i, h, cnt, flags, mn, mx, sum, sq);
+                load_record<WIDE>(R, i, h, cnt, flags, mn, mx, mo);
             }
         }
+        const double sum = mo.S1, sq = mo.S2;   // about the pivot mo.p0
         // need_adj: 0 every record is an edge (boundary maps), 1 keep edges seen
         // on a nearest-neighbour face, 2 keep all and carry the flag (partials)
         if (need_adj == 0) flags |= ADJ_FLAG;
@@ -318,7 +342,8 @@ __global__ __launch_bounds__(256) void k_reduce_edges(int64_t E, const uint32_t*
             w[42] = cnt | (flags & ADJ_FLAG);
             w[43] = mn;
             w[44] = mx;
-            w[45] = w[46] = w[47] = 0;
+            w[WREC_PIV] = __float_as_uint((float)mo.p0);   // a sample: exact in f32
+            w[46] = w[47] = 0;
 #pragma unroll
             for (int j = 0; j < WREC_WORDS / 4; ++j) p[j] = make_uint4(w[4 * j], w[4 * j + 1], w[4 * j + 2], w[4 * j + 3]);
             O.wsums[e] = make_double2(sum, sq);
@@ -338,12 +363,13 @@ __global__ __launch_bounds__(256) void k_reduce_edges(int64_t E, const uint32_t*
             return;
         }
         const double c = (double)cnt;
-        const double mean = sum / c;
-        // population variance from the f64 power sums: absolute error below
-        // ~(n + 2) eps max(x^2) (each x^2 of a float is exact in f64, the
-        // error is the accumulation's); an edge whose samples are all equal
-        // (min == max) has variance exactly 0, as the two-pass rule gives
-        double var = (sq - sum * mean) / c;
+        const double dm = sum / c;
+        const double mean = mo.p0 + dm;
+        // population variance from the sums about the pivot (a sample of the
+        // edge): the cancellation in S2 - S1 * (S1 / n) is bounded by the
+        // samples' spread, not by their magnitude; an edge whose samples are
+        // all equal (min == max) has variance exactly 0, as the two-pass rule
+        double var = (sq - sum * dm) / c;
         if (var < 0.0 || mn == mx) var = 0.0;
         const double vmin = (double)ord2f(mn), vmax = (double)ord2f(mx);
         double qv[5] = {0.0, 0.0, 0.0, 0.0, 0.0};   // registers (constant indices after unrolling)

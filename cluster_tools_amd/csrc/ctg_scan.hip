@@ -88,8 +88,9 @@ struct __align__(16) Table {
     uint64_t key[TABLE_CAP];
     double sum[TABLE_CAP];
     double sq[TABLE_CAP];
-    // hist words 0..20, 21 cnt|ADJ, 22 min, 23 max; odd row stride (25 words)
-    // so atomics to different entries spread over the LDS banks
+    // hist words 0..20, 21 cnt|ADJ, 22 min, 23 max, 24 pivot (the entry's
+    // first sample, claimed by CAS); odd row stride (25 words) so atomics to
+    // different entries spread over the LDS banks
     uint32_t w[TABLE_CAP][NREC_WORDS + 1];
     uint16_t compact[TABLE_CAP];
     uint32_t wave_cnt[WAVES];
@@ -109,7 +110,11 @@ __device__ __forceinline__ void entry_reset(Table& T, int e) {
     for (int j = 0; j < HWORDS + 1; ++j) T.w[e][j] = 0u;
     T.w[e][22] = ORD_POS_INF;
     T.w[e][23] = ORD_NEG_INF;
+    T.w[e][24] = PIV_EMPTY;
 }
+
+// pivot bits of a sample: its own bits, NaN -> 0 (never PIV_EMPTY)
+__device__ __forceinline__ uint32_t pivot_bits(float a) { return a == a ? __float_as_uint(a) : 0u; }
 
 // home bucket: four slots starting at a multiple of 4, read by two ds_read_b128
 // Two full-rate 24-bit multiplies (v_mul_u32_u24) instead of 32-bit ones and a
@@ -199,6 +204,9 @@ __device__ __noinline__ void table_flush_waves(Table& T, RecordBuf R, Counters* 
                 } else if (q < 7) {
                     const uint32_t* w = &T.w[e][4 * (q - 1)];
                     val = make_uint4(w[0], w[1], w[2], w[3]);
+                } else {   // word 28: the pivot (none: adjacency-only entry, no samples)
+                    const uint32_t pv = T.w[e][24];
+                    val.x = pv == PIV_EMPTY ? 0u : pv;
                 }
                 // histogram words 0..20 sit in pieces 1..5 and piece 6's .x
                 auto h2 = [](uint32_t v) { return (v & 0xFFFFu) + (v >> 16); };
@@ -219,9 +227,11 @@ __device__ __noinline__ void table_flush_waves(Table& T, RecordBuf R, Counters* 
 
 // One record straight to HBM: a key that found no room in the table.
 // sa / sb: histogram slots of the samples (-1: none); s / q / mn / mx: the
-// sum, sum of squares and ordered min / max this record carries.
+// shifted sum, sum of squares (about the pivot bits piv) and ordered min / max
+// this record carries.
 __device__ __noinline__ void emit_direct(RecordBuf R, Counters* C, uint64_t key, uint32_t cnt_flag, int sa, int sb,
-                                         double s, double q, uint32_t mn, uint32_t mx, bool with_stats) {
+                                         double s, double q, uint32_t mn, uint32_t mx, uint32_t piv,
+                                         bool with_stats) {
     const int reg = blockIdx.x & (NREG - 1);
     const unsigned long long j = atomicAdd(&C->rcount[reg], 1ull);
     atomicAdd(&C->n_direct, 1ull);
@@ -241,7 +251,8 @@ __device__ __noinline__ void emit_direct(RecordBuf R, Counters* C, uint64_t key,
     b[NREC_OFF + 21] = cnt_flag;
     b[NREC_OFF + 22] = mn;
     b[NREC_OFF + 23] = mx;
-    for (int j = NREC_OFF + NREC_WORDS; j < NREC_STRIDE; ++j) b[j] = 0u;
+    b[NREC_PIV] = piv;
+    for (int j = NREC_PIV + 1; j < NREC_STRIDE; ++j) b[j] = 0u;
 }
 
 template <typename DataT>
@@ -322,15 +333,16 @@ __device__ __forceinline__ int bucket_match(const uint4& b01, const uint4& b23, 
     return s;
 }
 
-// statistics of one staged entry into table slot s (s < 0: direct record)
+// statistics of one staged entry into table slot s (s < 0: direct record);
+// pv: the slot's pivot word as read by the batch (PIV_EMPTY: none yet)
 template <int MODE, bool FAST40, bool BATCH, typename StageT>
-__device__ __forceinline__ void fold_stats(Table& T, const StageT& e, int s, RecordBuf R, Counters* C, double scale,
-                                           double offset, bool& need, int ablate) {
+__device__ __forceinline__ void fold_stats(Table& T, const StageT& e, int s, uint32_t pv, RecordBuf R, Counters* C,
+                                           double scale, double offset, bool& need, int ablate) {
     constexpr bool BND = MODE == MODE_BOUNDARY;
     constexpr bool AFF = MODE == MODE_AFFINITY;
     const uint64_t key = ((uint64_t)e.x << 32) | e.y;
     if constexpr (MODE == MODE_GRAPH) {
-        if (s < 0) emit_direct(R, C, key, 0u, -1, -1, 0.0, 0.0, 0u, 0u, false);
+        if (s < 0) emit_direct(R, C, key, 0u, -1, -1, 0.0, 0.0, 0u, 0u, 0u, false);
         return;
     } else {
         // adjacency-only entries: a nearest-neighbour face of an affinity map, or
@@ -348,12 +360,13 @@ __device__ __forceinline__ void fold_stats(Table& T, const StageT& e, int s, Rec
         const double da = (double)a, db = (double)b;
         const int sa = adj ? -1 : sample_slot<FAST40>(da, scale, offset);
         const int sb = (two && !adj) ? sample_slot<FAST40>(db, scale, offset) : -1;
-        const double ds = two ? da + db : da;
-        const double dq = two ? da * da + db * db : da * da;
         const uint32_t mn = f2ord(fminf(a, b)), mx = f2ord(fmaxf(a, b));
-        if (s < 0) {
-            emit_direct(R, C, key, n | (adj ? ADJ_FLAG : nnf), sa, sb, adj ? 0.0 : ds, adj ? 0.0 : dq,
-                        adj ? ORD_POS_INF : mn, adj ? ORD_NEG_INF : mx, true);
+        const uint32_t mine = pivot_bits(a);
+        if (s < 0) {   // a direct record is its own entry: pivot = its first sample
+            const double ea = da - (double)__uint_as_float(mine), eb = db - (double)__uint_as_float(mine);
+            emit_direct(R, C, key, n | (adj ? ADJ_FLAG : nnf), sa, sb, adj ? 0.0 : (two ? ea + eb : ea),
+                        adj ? 0.0 : (two ? ea * ea + eb * eb : ea * ea), adj ? ORD_POS_INF : mn,
+                        adj ? ORD_NEG_INF : mx, adj ? 0u : mine, true);
             return;
         }
         if (adj) {
@@ -364,19 +377,31 @@ __device__ __forceinline__ void fold_stats(Table& T, const StageT& e, int s, Rec
             if (s == 0x7FFFFFF) atomicAdd(&C->pad[1], 1ull);
             return;
         }
-        // fire-and-forget adds: the per-wave sample budget (k_face_scan) keeps
-        // every count, hence every u16 histogram slot, below 2^16
-        atomicAdd(&T.sum[s], ds);
-        atomicAdd(&T.sq[s], dq);
+        // fire-and-forget updates: the per-wave sample budget (k_face_scan)
+        // keeps every count, hence every u16 histogram slot, below 2^16.  The
+        // ones that do not need the pivot go first, so the batch's pivot reads
+        // land behind them.
         atomicMin(&T.w[s][22], mn);
         atomicMax(&T.w[s][23], mx);
         // word 21 carries only the ADJ flag in the table; the count is the
         // histogram's sum, filled in by the flush
         if (nnf) atomicOr(&T.w[s][21], ADJ_FLAG);
-        if (ablate & 128) return;   // diagnostic: no histogram
-        if constexpr (BND) hist_add2(T, s, sa, sb);
-        else if (two) hist_add2(T, s, sa, sb);
-        else atomicAdd(&T.w[s][sa >> 1], 1u << ((sa & 1) * 16));
+        if (!(ablate & 128)) {   // diagnostic 128: no histogram
+            if constexpr (BND) hist_add2(T, s, sa, sb);
+            else if (two) hist_add2(T, s, sa, sb);
+            else atomicAdd(&T.w[s][sa >> 1], 1u << ((sa & 1) * 16));
+        }
+        // the entry's pivot: the first sample that claims the empty pivot word
+        // (a CAS, so every lane of every wave agrees on it; the word is reset
+        // only inside a flush, between two workgroup barriers)
+        if (pv == PIV_EMPTY) {
+            const uint32_t old = atomicCAS(&T.w[s][24], PIV_EMPTY, mine);
+            pv = old == PIV_EMPTY ? mine : old;
+        }
+        const double dp = (double)__uint_as_float(pv);
+        const double ea = da - dp, eb = db - dp;
+        atomicAdd(&T.sum[s], two ? ea + eb : ea);
+        atomicAdd(&T.sq[s], two ? ea * ea + eb * eb : ea * ea);
     }
 }
 
@@ -403,6 +428,7 @@ __device__ __forceinline__ void fold_batch(Table& T, const StageT* __restrict__ 
         b01[i] = *reinterpret_cast<const uint4*>(&T.key[h[i]]);
         b23[i] = *reinterpret_cast<const uint4*>(&T.key[h[i] + 2]);
     }
+    int slot[NPER];
 #pragma unroll
     for (int i = 0; i < NPER; ++i) {
         const bool valid = lane + WAVE * i < nb;
@@ -430,8 +456,20 @@ __device__ __forceinline__ void fold_batch(Table& T, const StageT* __restrict__ 
                 }
             }
         }
-        if (valid) fold_stats<MODE, FAST40, BATCH, StageT>(T, e[i], s, R, C, scale, offset, need, ablate);
+        slot[i] = s;
     }
+    // the entries' pivot words, read together (one LDS round trip for the batch)
+    uint32_t pv[NPER];
+#pragma unroll
+    for (int i = 0; i < NPER; ++i) {
+        pv[i] = PIV_EMPTY;
+        if (MODE != MODE_GRAPH && slot[i] >= 0)
+            pv[i] = __hip_atomic_load(&T.w[slot[i]][24], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+#pragma unroll
+    for (int i = 0; i < NPER; ++i)
+        if (lane + WAVE * i < nb)
+            fold_stats<MODE, FAST40, BATCH, StageT>(T, e[i], slot[i], pv[i], R, C, scale, offset, need, ablate);
 }
 
 // diagnostic time stamp (volatile: never merged or moved across other code)

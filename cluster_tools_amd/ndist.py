@@ -37,9 +37,10 @@ from . import rag
 from .blocking import blocking
 
 N_FEATURES = 10
-# companion varlen dataset of sub_features (uint32): per edge the (sum, sumsq)
-# float64 pair as 4 words, then the 48 words of the wide statistics record
-# (42 histogram slots, count|ADJ, ordered min, ordered max, pad) = 208 B
+# companion varlen dataset of sub_features (uint32): per edge the shifted sums
+# (S1, S2) about a pivot p as 4 words, then the 48 words of the wide statistics
+# record (42 histogram slots, count|ADJ, ordered min, ordered max, pivot p as
+# float32 bits, 2 zero words) = 208 B (include/ctg.h, ctg_merge_stats)
 STATS_SUFFIX = '_stats'
 STATS_WORDS = 4 + rag.WIDE_WORDS
 ORD_POS_INF = 0xFF800000   # order-preserving u32 code of +inf (ctg_internal.h f2ord)

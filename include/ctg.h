@@ -149,9 +149,13 @@ int ctg_unique_labels(const uint64_t* labels, const int64_t* shape,
 int ctg_unique_values(const uint64_t* values, int64_t n, int mem, void* stream, ctg_result** out);
 
 /* Combine partial statistics tables (wide records, one per (part, edge)) into
- * one table: counts add, sums add, min/max elementwise, histograms add.
- *   keys     n x 2 uint64 (u,v) per record; sums n x 2 float64 (sum, sumsq);
- *   records  n x CTG_WIDE_RECORD_WORDS uint32. */
+ * one table: counts add, moments combine exactly (re-pivoted shifted sums,
+ * i.e. Chan's pairwise rule), min/max elementwise, histograms add.
+ *   keys     n x 2 uint64 (u,v) per record;
+ *   sums     n x 2 float64 (S1, S2) = (sum(x - p), sum((x - p)^2)) about the
+ *            record's pivot p = the float32 in record word 45 (0: power sums);
+ *   records  n x CTG_WIDE_RECORD_WORDS uint32: 42 histogram slots, count|ADJ,
+ *            ordered min, ordered max, pivot bits, 2 zero words. */
 int ctg_merge_stats(const uint64_t* keys, const double* sums, const uint32_t* records,
                     int64_t n, double hist_lo, double hist_hi, int keep_stats,
                     int mem, void* stream, ctg_result** out);

@@ -27,27 +27,35 @@ def ord2f(o):
 
 
 def encode_stats(stats):
-    """oracle _accumulate stats -> (sums (E,2) f64, records (E,48) u32)."""
+    """oracle _accumulate stats -> (sums (E,2) f64, records (E,48) u32): the
+    shifted sums (S1, S2) about the pivot p = float32(mean) in word 45."""
     c = stats['count'].astype(np.float64)
     n = c.shape[0]
-    sums = np.zeros((n, 2))
-    sums[:, 0] = stats['sum']
     with np.errstate(invalid='ignore', divide='ignore'):
-        sums[:, 1] = stats['m2'] + np.where(c > 0, stats['sum'] ** 2 / np.maximum(c, 1), 0.0)
+        mean = np.where(c > 0, stats['sum'] / np.maximum(c, 1), 0.0)
+    p = mean.astype(np.float32)
+    sums = np.zeros((n, 2))
+    sums[:, 0] = stats['sum'] - c * p.astype(np.float64)
+    with np.errstate(invalid='ignore', divide='ignore'):
+        sums[:, 1] = stats['m2'] + np.where(c > 0, sums[:, 0] ** 2 / np.maximum(c, 1), 0.0)
     rec = np.zeros((n, WIDE), dtype=np.uint32)
     rec[:, :O.NBINS + 2] = stats['hist'].astype(np.uint32)
     rec[:, 42] = stats['count'].astype(np.uint32) | ADJ
     rec[:, 43] = f2ord(stats['min'])
     rec[:, 44] = f2ord(stats['max'])
+    rec[:, 45] = p.view(np.uint32)
     return sums, rec
 
 
 def decode_stats(sums, rec):
     c = (rec[:, 42] & np.uint32(0x7FFFFFFF)).astype(np.int64)
-    s = sums[:, 0]
+    p = rec[:, 45].view(np.float32).astype(np.float64)
+    s1 = sums[:, 0]
     with np.errstate(invalid='ignore', divide='ignore'):
-        mean = np.where(c > 0, s / np.maximum(c, 1), 0.0)
-    m2 = sums[:, 1] - np.where(c > 0, s * s / np.maximum(c, 1), 0.0)
+        d = np.where(c > 0, s1 / np.maximum(c, 1), 0.0)
+    mean = np.where(c > 0, p + d, 0.0)
+    s = np.where(c > 0, mean * c, 0.0)
+    m2 = sums[:, 1] - np.where(c > 0, s1 * d, 0.0)
     return dict(count=c, sum=s, mean=mean, m2=m2,
                 min=ord2f(rec[:, 43]).astype(np.float64), max=ord2f(rec[:, 44]).astype(np.float64),
                 hist=rec[:, :O.NBINS + 2].astype(np.int64))

@@ -103,28 +103,37 @@ def _reference_boundary(lab, bnd, with_samples=False):
     del keys
     inv2 = torch.cat([inv, inv])
     del inv
-    E = uk.shape[0]
-    s = torch.zeros(E, dtype=torch.float64, device=lab.device).scatter_add_(0, inv2, x)
-    q = torch.zeros(E, dtype=torch.float64, device=lab.device).scatter_add_(0, inv2, x * x)
-    mn = torch.full((E,), float('inf'), dtype=torch.float64, device=lab.device).scatter_reduce_(
-        0, inv2, x, 'amin')
-    mx = torch.full((E,), float('-inf'), dtype=torch.float64, device=lab.device).scatter_reduce_(
-        0, inv2, x, 'amax')
+    stats = _moments(uk.shape[0], inv2, x, 2 * cnt)
     if with_samples:
-        return (uk, 2 * cnt, s, q, mn, mx), (inv2, x)
-    return uk, 2 * cnt, s, q, mn, mx
+        return (uk, 2 * cnt) + stats, (inv2, x)
+    return (uk, 2 * cnt) + stats
 
 
-def _check(res, uk, cnt, s, q, mn, mx):
+def _moments(E, inv, x, cnt):
+    """Two-pass per-edge moments of the enumerated samples: (sum, M2, min,
+    max), M2 = sum((x - mean)^2) -- the reference the variance is held to at
+    rtol 1e-5 with no absolute slack."""
+    dev = inv.device
+    s = torch.zeros(E, dtype=torch.float64, device=dev).scatter_add_(0, inv, x)
+    mean = s / cnt
+    d = x - mean[inv]
+    m2 = torch.zeros(E, dtype=torch.float64, device=dev).scatter_add_(0, inv, d * d)
+    del d
+    mn = torch.full((E,), float('inf'), dtype=torch.float64, device=dev).scatter_reduce_(0, inv, x, 'amin')
+    mx = torch.full((E,), float('-inf'), dtype=torch.float64, device=dev).scatter_reduce_(0, inv, x, 'amax')
+    return s, m2, mn, mx
+
+
+def _check(res, uk, cnt, s, m2, mn, mx):
     e = res.edges_torch_i64()
     f = res.features_torch()
     assert e.shape[0] == uk.shape[0]
     assert torch.equal(e[:, 0] * (1 << 32) + e[:, 1], uk)                # sorted unique keys, bit-exact
     assert torch.equal(f[:, 9], cnt.double())                             # counts bit-exact
     mean = s / cnt
-    var = torch.clamp(q / cnt - mean * mean, min=0.0)
-    assert torch.allclose(f[:, 0], mean, rtol=RTOL, atol=1e-12)
-    assert torch.allclose(f[:, 1], var, rtol=RTOL, atol=1e-9)
+    var = torch.where(mn == mx, torch.zeros_like(m2), m2 / cnt)          # all samples equal: exactly 0
+    assert torch.allclose(f[:, 0], mean, rtol=RTOL, atol=0.0)
+    assert torch.allclose(f[:, 1], var, rtol=RTOL, atol=0.0)
     assert torch.equal(f[:, 2], mn)
     assert torch.equal(f[:, 8], mx)
     qs = f[:, 2:9]                                                        # min, q10..q90, max
@@ -160,42 +169,126 @@ def test_configs4_fragmented_full_size():
     res.free()
 
 
+def _pair_keys(a, b):
+    m = a != b
+    return torch.minimum(a[m], b[m]) * (1 << 32) + torch.maximum(a[m], b[m]), m
+
+
+def _rag_keys_chunked(lab, chunk=128):
+    """Sorted unique (u << 32 | v) keys of every boundary face (the
+    nearest-neighbour RAG), enumerated per z-chunk with torch comparisons."""
+    Z = lab.shape[0]
+    parts = []
+    for z0 in range(0, Z, chunk):
+        z1 = min(Z, z0 + chunk)
+        sl = lab[z0:z1]
+        ks = [_pair_keys(sl[:, :, :-1], sl[:, :, 1:])[0], _pair_keys(sl[:, :-1], sl[:, 1:])[0]]
+        zt = min(z1, Z - 1)
+        if zt > z0:
+            ks.append(_pair_keys(lab[z0:zt], lab[z0 + 1:zt + 1])[0])
+        parts.append(torch.unique(torch.cat(ks)))
+        del ks
+    return torch.unique(torch.cat(parts))
+
+
+def _reference_affinity(lab, affs, offsets, graph, n_pick=N_QSAMPLE, seed=0, chunk=128):
+    """SURVEY A.4 by torch, in z-chunks (memory bound independent of the
+    volume): sample aff[c, p] for q = p + o_c inside the volume with
+    L[p] != L[q] and (min, max) an edge of ``graph`` (sorted RAG keys).
+    Two passes: counts / sums / min / max, then M2 about the mean and the
+    exact 42-slot histograms of n_pick random edges.  Returns the expected
+    (uk, cnt, s, m2, mn, mx) over the edges that got a sample, the picked
+    rows (in uk order) and their histograms."""
+    Z, Y, X = lab.shape
+    E = graph.shape[0]
+    dev = lab.device
+    cnt = torch.zeros(E, dtype=torch.int64, device=dev)
+    s = torch.zeros(E, dtype=torch.float64, device=dev)
+    mn = torch.full((E,), float('inf'), dtype=torch.float64, device=dev)
+    mx = torch.full((E,), float('-inf'), dtype=torch.float64, device=dev)
+    m2 = torch.zeros(E, dtype=torch.float64, device=dev)
+
+    def samples():
+        for c, (oz, oy, ox) in enumerate(offsets):
+            py = slice(max(0, -oy), Y - max(0, oy))
+            px = slice(max(0, -ox), X - max(0, ox))
+            qy = slice(py.start + oy, py.stop + oy)
+            qx = slice(px.start + ox, px.stop + ox)
+            zlo, zhi = max(0, -oz), Z - max(0, oz)
+            for z0 in range(zlo, zhi, chunk):
+                z1 = min(zhi, z0 + chunk)
+                k, m = _pair_keys(lab[z0:z1, py, px], lab[z0 + oz:z1 + oz, qy, qx])
+                idx = torch.searchsorted(graph, k).clamp_(max=E - 1)
+                hit = graph[idx] == k
+                yield idx[hit], affs[c, z0:z1, py, px][m][hit].double()
+
+    for idx, x in samples():
+        cnt.scatter_add_(0, idx, torch.ones_like(idx))
+        s.scatter_add_(0, idx, x)
+        mn.scatter_reduce_(0, idx, x, 'amin')
+        mx.scatter_reduce_(0, idx, x, 'amax')
+    present = cnt > 0
+    row = torch.cumsum(present.to(torch.int64), 0) - 1
+    mean = s / cnt.clamp(min=1)
+    g = torch.Generator(device='cpu').manual_seed(seed)
+    pres_ids = torch.nonzero(present).flatten()
+    pick = pres_ids[torch.randperm(pres_ids.shape[0], generator=g)[:n_pick].to(dev)]
+    where = torch.full((E,), -1, dtype=torch.int64, device=dev)
+    where[pick] = torch.arange(pick.shape[0], device=dev)
+    h = torch.zeros(pick.shape[0] * 42, dtype=torch.int64, device=dev)
+    for idx, x in samples():
+        d = x - mean[idx]
+        m2.scatter_add_(0, idx, d * d)
+        sel = where[idx]
+        k = sel >= 0
+        h += torch.bincount(sel[k] * 42 + _slots(x[k]), minlength=h.shape[0])
+    ref = (graph[present], cnt[present], s[present], m2[present], mn[present], mx[present])
+    return ref, row[pick], h.reshape(-1, 42).cpu().numpy()
+
+
+def _check_quantile_rows(f, rows, h):
+    fs = f[rows].cpu().numpy()
+    assert np.array_equal(h.sum(axis=1), fs[:, 9].astype(np.int64))
+    worst = 0.0
+    for i in range(fs.shape[0]):
+        q = O.vigra_quantiles(h[i], fs[i, 2], fs[i, 8], fs[i, 9], 0.0, 1.0)
+        worst = max(worst, float(np.abs(q[1:6] - fs[i, 3:8]).max()))
+    assert worst <= 1e-9, worst
+
+
+def _affinity_full_size(shape, offsets, seed):
+    lab, bnd = rag.synth_volume(shape, cell=10, seed=seed)
+    affs = rag.synth_affinities(bnd, offsets)
+    del bnd
+    res = rag.rag_features_handle(lab, affs, offsets=offsets)
+    graph = _rag_keys_chunked(lab)
+    ref, rows, h = _reference_affinity(lab, affs, offsets, graph, seed=seed)
+    del lab, affs, graph
+    _check(res, *ref)
+    _check_quantile_rows(res.features_torch(), rows, h)
+    res.free()
+    return ref[0].shape[0]
+
+
 def test_configs3_long_range_affinities_edge_filter():
     """BASELINE configs[3] offsets (12 long-range channels) at 512^3: a sample
     aff[c,p] counts iff L[p] != L[p+o_c] and (min,max) is an edge of the
     nearest-neighbour RAG."""
-    shape = (512, 512, 512)
-    lab, bnd = rag.synth_volume(shape, cell=10, seed=5)
-    affs = rag.synth_affinities(bnd, S.LR_OFFSETS)
-    res = rag.rag_features_handle(lab, affs, offsets=S.LR_OFFSETS)
-    graph = torch.unique(torch.cat([_faces(lab, bnd, ax)[0] for ax in range(3)]))
-    keys, vals = [], []
-    Z, Y, X = shape
-    for c, (oz, oy, ox) in enumerate(S.LR_OFFSETS):
-        pz = slice(max(0, -oz), Z - max(0, oz))
-        py = slice(max(0, -oy), Y - max(0, oy))
-        px = slice(max(0, -ox), X - max(0, ox))
-        qz = slice(pz.start + oz, pz.stop + oz)
-        qy = slice(py.start + oy, py.stop + oy)
-        qx = slice(px.start + ox, px.stop + ox)
-        a, b = lab[pz, py, px], lab[qz, qy, qx]
-        m = a != b
-        k = torch.minimum(a[m], b[m]) * (1 << 32) + torch.maximum(a[m], b[m])
-        x = affs[c][pz, py, px][m].double()
-        keep = torch.isin(k, graph)
-        keys.append(k[keep])
-        vals.append(x[keep])
-    keys = torch.cat(keys)
-    x = torch.cat(vals)
-    uk, inv, cnt = torch.unique(keys, return_inverse=True, return_counts=True)
-    E = uk.shape[0]
-    s = torch.zeros(E, dtype=torch.float64, device=lab.device).scatter_add_(0, inv, x)
-    q = torch.zeros(E, dtype=torch.float64, device=lab.device).scatter_add_(0, inv, x * x)
-    mn = torch.full((E,), float('inf'), dtype=torch.float64, device=lab.device).scatter_reduce_(0, inv, x, 'amin')
-    mx = torch.full((E,), float('-inf'), dtype=torch.float64, device=lab.device).scatter_reduce_(0, inv, x, 'amax')
-    _check(res, uk, cnt, s, q, mn, mx)
-    _check_quantiles(res.features_torch(), inv, x, seed=3)
-    res.free()
+    _affinity_full_size((512, 512, 512), S.LR_OFFSETS, seed=5)
+
+
+@pytest.mark.timeout(400)
+def test_configs3_1024_nearest_neighbour_affinities_full_size():
+    """BASELINE configs[3] at its stated size: 1024^3, the 3 nearest-neighbour
+    channels of test_edge_features.py:26."""
+    assert _affinity_full_size((1024, 1024, 1024), S.NN_OFFSETS, seed=6) > 7_000_000
+
+
+@pytest.mark.timeout(400)
+def test_configs3_1024_long_range_affinities_full_size():
+    """BASELINE configs[3] at its stated size: 1024^3 with the 12 offsets of
+    test/mutex_watershed/test_mws.py:26-29 (48 GB of affinities)."""
+    assert _affinity_full_size((1024, 1024, 1024), S.LR_OFFSETS, seed=7) > 7_000_000
 
 
 # ---------------------------------------------------------------- configs[2]: 2048^3

@@ -20,25 +20,17 @@ pytestmark = pytest.mark.gpu
 RTOL = 1e-5
 ATOL = 0.0
 BIN = 1.0 / 40
-EPS = np.finfo(np.float64).eps
-
-
-def var_bound(f):
-    """Per-edge absolute error bound of the one-pass f64 variance (sum of
-    squares minus sum times mean): (n + 2) eps max(x^2)."""
-    return (f[:, 9] + 2) * EPS * np.maximum(f[:, 2] ** 2, f[:, 8] ** 2)
 GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'golden')
 
 
 def check_features(f_gpu, f_ref):
+    """north_star bars with no absolute slack: mean / var / min / max within
+    1e-5 relative (the variance too: the GPU keeps shifted sums about a
+    per-edge pivot), counts exact, quantiles within one bin."""
     assert f_gpu.shape == f_ref.shape
     np.testing.assert_array_equal(f_gpu[:, 9], f_ref[:, 9])            # count exact
-    for c in (0, 2, 8):                                                  # mean min max
+    for c in (0, 1, 2, 8):                                               # mean var min max
         np.testing.assert_allclose(f_gpu[:, c], f_ref[:, c], rtol=RTOL, atol=ATOL)
-    # variance: rtol 1e-5, or within the one-pass formula's error bound where
-    # that is larger (edges with var below ~1e11 eps max(x^2))
-    err = np.abs(f_gpu[:, 1] - f_ref[:, 1])
-    assert np.all(err <= np.maximum(RTOL * np.abs(f_ref[:, 1]), var_bound(f_ref))), err.max()
     np.testing.assert_array_less(np.abs(f_gpu[:, 3:8] - f_ref[:, 3:8]), BIN + 1e-12)
 
 
@@ -471,7 +463,8 @@ def test_merge_and_pairs_above_2_32(gpu):
 
 def test_variance_constant_and_near_constant_edges(gpu):
     """Edges whose samples are all equal have variance exactly 0; near-constant
-    edges (spread 1e-3 around 0.75) meet rtol 1e-5 against the two-pass oracle."""
+    edges (spread 1e-3 around 0.75, and around 1000) meet rtol 1e-5 against
+    the two-pass oracle."""
     rng = np.random.default_rng(11)
     lab = np.zeros((24, 40, 72), np.uint64)
     lab[:, :, 36:] = 1
@@ -487,6 +480,21 @@ def test_variance_constant_and_near_constant_edges(gpu):
     assert np.all(f[const, 1] == 0.0)
     np.testing.assert_allclose(f[~const, 1], f_ref[~const, 1], rtol=RTOL, atol=0)
     np.testing.assert_allclose(f[:, 0], f_ref[:, 0], rtol=1e-12, atol=0)
+    # spread 1e-3 around 1000 (outside the histogram range): var / mean^2 ~ 1e-13,
+    # where power sums (sum x^2 - sum x * mean) lose every digit; the pivoted
+    # sums keep rtol 1e-5, in the scan and through the statistics merge
+    big = (1000.0 + 1e-3 * rng.random(lab.shape)).astype(np.float32)
+    out = rag.rag_features(lab, big, keep_stats=True)
+    e_ref, f_ref = O.boundary_features(lab, big)
+    np.testing.assert_array_equal(out['edges'], e_ref)
+    check_features(out['features'], f_ref)
+    assert np.all(f_ref[:, 1] > 0)
+    a = rag.rag_features(lab[:11], big[:11], keep_stats=True)
+    b = rag.rag_features(lab[10:], big[10:], own_begin=(1, 0, 0), keep_stats=True)
+    m = rag.merge_stats(np.concatenate([a['edges'], b['edges']]), np.concatenate([a['sums'], b['sums']]),
+                        np.concatenate([a['records'], b['records']]))
+    np.testing.assert_array_equal(m['edges'], e_ref)
+    check_features(m['features'], f_ref)
 
 
 def test_bucket_sort_skewed_keys(gpu, monkeypatch):
