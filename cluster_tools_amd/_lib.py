@@ -31,6 +31,7 @@ CTG_IO_ZARR_DOT = 1
 CTG_IO_ZARR_SLASH = 2
 CTG_IO_RAW = 0
 CTG_IO_GZIP = 1
+CTG_IO_ZLIB = 2
 
 _lock = threading.Lock()
 _lib = None
@@ -84,11 +85,12 @@ PROTOTYPES = {
     'ctg_sym_eigenvalues': (ctypes.c_int, [c_vp, ctypes.c_int, ctypes.c_int64, c_vp, c_vp]),
     'ctg_trim': (ctypes.c_int, []),
     'ctg_io_read_box': (ctypes.c_int, [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
-                                       c_vp, c_vp, ctypes.c_int, c_vp, c_vp, c_vp, ctypes.c_int]),
+                                       c_vp, c_vp, ctypes.c_int, c_vp, c_vp, c_vp, ctypes.c_int, c_vp]),
     'ctg_io_read_varlen': (ctypes.c_int, [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.c_int64, c_vp,
                                           ctypes.c_int, c_vp, c_vp, ctypes.c_int]),
     'ctg_io_free': (None, [c_vp]),
     'ctg_io_cache_clear': (None, []),
+    'ctg_io_cache_drop': (None, [ctypes.c_char_p]),
     'ctg_io_write_chunks': (ctypes.c_int, [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                            ctypes.c_int64, c_vp, c_vp, c_vp, c_vp, ctypes.c_int, ctypes.c_int,
                                            ctypes.c_int, ctypes.c_int]),

@@ -635,6 +635,32 @@ struct DensePairs {
     }
 };
 
+// The dense relabellings below map a label to its rank in the sorted unique
+// label table U.  The reduce recognises the ignore label as dense id 0, so with
+// ignore_label set the table must start with label 0 even where the array
+// holds no 0 -- else the smallest real label would become 0 and its edges
+// would be dropped.  Puts a 0 in front of U->nodes when U[0] != 0.
+static int keep_zero_first(ctg_result* U, hipStream_t s) {
+    uint64_t first = 0;
+    if (U->n_nodes > 0) {
+        CTG_CHECK(hipMemcpyAsync(&first, U->nodes, 8, hipMemcpyDeviceToHost, s));
+        CTG_CHECK(hipStreamSynchronize(s));
+    }
+    if (U->n_nodes > 0 && first == 0) return CTG_OK;
+    uint64_t* t = (uint64_t*)dalloc((size_t)(U->n_nodes + 1) * 8);
+    if (!t) {
+        set_error("out of device memory for the dense relabelling table");
+        return CTG_ERR_NOMEM;
+    }
+    CTG_CHECK(hipMemsetAsync(t, 0, 8, s));
+    if (U->n_nodes)
+        CTG_CHECK(hipMemcpyAsync(t + 1, U->nodes, (size_t)U->n_nodes * 8, hipMemcpyDeviceToDevice, s));
+    dfree(U->nodes);   // stream-ordered reuse
+    U->nodes = t;
+    U->n_nodes += 1;
+    return CTG_OK;
+}
+
 // Labels >= 2^32: the face keys pack (u,v) as 32+32 bits, so the
 // array is relabelled densely through its sorted unique labels (a monotone
 // map: sorted dense edges stay sorted), scanned as 32-bit labels, and the
@@ -647,6 +673,10 @@ static int rag_dense_relabel(const void* dl, const void* dd, int data_kind, int 
     ctg_result* U = nullptr;
     int rc = ctg_unique_labels((const uint64_t*)dl, shape, nullptr, nullptr, CTG_MEM_DEVICE, stream, &U);
     if (rc) return rc;
+    if (ignore_label && (rc = keep_zero_first(U, s)) != CTG_OK) {
+        ctg_free(U);
+        return rc;
+    }
     if (U->n_nodes > 0xFFFFFFFFll) {
         ctg_free(U);
         set_error("ctg_rag_features: more than 2^32 distinct labels in one array");
@@ -1190,6 +1220,10 @@ int ctg_rag_blocks(const void* labels, int label_bits, const void* data, int dat
         ctg_result* U = nullptr;
         rc = ctg_unique_values(l64, labels_len, CTG_MEM_DEVICE, stream, &U);
         if (rc) return rc;
+        if (ignore_label && (rc = keep_zero_first(U, s)) != CTG_OK) {
+            ctg_free(U);
+            return rc;
+        }
         if (U->n_nodes > (int64_t)(1ull << P.tag_shift)) {
             ctg_free(U);
             set_error("ctg_rag_blocks: too many distinct labels for one batch of blocks: call with fewer blocks");

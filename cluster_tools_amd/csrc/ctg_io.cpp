@@ -185,7 +185,9 @@ void parallel_for(int64_t n, int n_threads, F&& f) {
 // CTG_IO_CACHE_MB, default 4096; 0 disables), so every chunk is inflated
 // once per pass whatever the block order; concurrent readers of one chunk
 // wait for the first one's decode.  An entry is reused only while the file's
-// size and mtime are unchanged, and native writes drop it.
+// inode, size, mtime and ctime are unchanged (every writer here replaces a
+// chunk file by rename, so a rewrite always shows as a new inode), and native
+// writes -- and the Python writers, through ctg_io_cache_drop -- drop it.
 // ---------------------------------------------------------------------------
 struct Chunk {
     int64_t dims[MAXD];
@@ -193,10 +195,18 @@ struct Chunk {
 };
 using ChunkPtr = std::shared_ptr<const Chunk>;
 
+struct Stamp {
+    int64_t mtime_ns = 0, ctime_ns = 0, size = -1;
+    uint64_t ino = 0, dev = 0;
+    bool operator==(const Stamp& o) const {
+        return mtime_ns == o.mtime_ns && ctime_ns == o.ctime_ns && size == o.size && ino == o.ino && dev == o.dev;
+    }
+};
+
 struct CacheEntry {
     std::shared_future<ChunkPtr> fut;
     bool ready = false;
-    int64_t mtime_ns = 0, fsize = -1;
+    Stamp stamp;
     size_t bytes = 0;
     std::list<std::string>::iterator lru;
 };
@@ -214,11 +224,14 @@ size_t cache_budget() {
     return b;
 }
 
-bool file_stamp(const std::string& path, int64_t& mtime_ns, int64_t& size) {
+bool file_stamp(const std::string& path, Stamp& s) {
     struct stat st;
     if (stat(path.c_str(), &st) != 0) return false;
-    mtime_ns = (int64_t)st.st_mtim.tv_sec * 1000000000ll + st.st_mtim.tv_nsec;
-    size = (int64_t)st.st_size;
+    s.mtime_ns = (int64_t)st.st_mtim.tv_sec * 1000000000ll + st.st_mtim.tv_nsec;
+    s.ctime_ns = (int64_t)st.st_ctim.tv_sec * 1000000000ll + st.st_ctim.tv_nsec;
+    s.size = (int64_t)st.st_size;
+    s.ino = (uint64_t)st.st_ino;
+    s.dev = (uint64_t)st.st_dev;
     return true;
 }
 
@@ -268,7 +281,7 @@ ChunkPtr decode_chunk(const std::string& path, int format, int ndim, const int64
     size_t n_el = 1;
     for (int a = 0; a < ndim; ++a) n_el *= (size_t)c->dims[a];
     c->data.resize(n_el * es);
-    if (compression == CTG_IO_GZIP) {
+    if (compression != CTG_IO_RAW) {   // gzip or zlib stream (auto-detected)
         if (!inflate_all(file.data() + off, file.size() - off, c->data.data(), c->data.size())) {
             *err = "corrupt compressed chunk " + path;
             return nullptr;
@@ -292,8 +305,8 @@ ChunkPtr get_chunk(const std::string& path, int format, int ndim, const int64_t*
                    int compression, bool* missing, std::string* err) {
     const size_t budget = cache_budget();
     if (budget == 0) return decode_chunk(path, format, ndim, chunks, es, swap, compression, missing, err);
-    int64_t mt = 0, sz = -1;
-    if (!file_stamp(path, mt, sz)) {
+    Stamp st;
+    if (!file_stamp(path, st)) {
         *missing = errno == ENOENT;
         if (!*missing) *err = "cannot stat " + path;
         return nullptr;
@@ -308,7 +321,7 @@ ChunkPtr get_chunk(const std::string& path, int format, int ndim, const int64_t*
             CacheEntry& e = it->second;
             if (!e.ready) {
                 wait_for = e.fut;
-            } else if (e.mtime_ns == mt && e.fsize == sz) {
+            } else if (e.stamp == st) {
                 g_lru.splice(g_lru.begin(), g_lru, e.lru);
                 return e.fut.get();
             } else {   // the file changed: decode again
@@ -320,8 +333,7 @@ ChunkPtr get_chunk(const std::string& path, int format, int ndim, const int64_t*
         if (!wait_for.valid()) {
             CacheEntry e;
             e.fut = prom.get_future().share();
-            e.mtime_ns = mt;
-            e.fsize = sz;
+            e.stamp = st;
             g_cache.emplace(key, e);
         }
     }
@@ -370,7 +382,7 @@ extern "C" {
 
 int ctg_io_read_box(const char* ds_path, int format, int dtype_size, int big_endian, int ndim, const int64_t* shape,
                     const int64_t* chunks, int compression, const int64_t* begin, const int64_t* end, void* out,
-                    int n_threads) {
+                    int n_threads, const void* fill_value) {
     if (!ds_path || !shape || !chunks || !begin || !end || check_geometry(ndim, shape, chunks, dtype_size)) {
         ctg::set_error("ctg_io_read_box: bad arguments");
         return CTG_ERR_ARG;
@@ -443,8 +455,13 @@ int ctg_io_read_box(const char* ds_path, int format, int dtype_size, int big_end
                 const int64_t ci2 = (a == L ? lo[L] : idx[a]) - cb[a];
                 s = s * (missing ? 1 : dims[a]) + (missing ? 0 : ci2);
             }
-            if (missing) std::memset(dst0 + (size_t)o * es, 0, (size_t)row * es);
-            else std::memcpy(dst0 + (size_t)o * es, payload + (size_t)s * es, (size_t)row * es);
+            if (missing && !fill_value) {
+                std::memset(dst0 + (size_t)o * es, 0, (size_t)row * es);
+            } else if (missing) {   // the array's fill value
+                for (int64_t k = 0; k < row; ++k) std::memcpy(dst0 + (size_t)(o + k) * es, fill_value, es);
+            } else {
+                std::memcpy(dst0 + (size_t)o * es, payload + (size_t)s * es, (size_t)row * es);
+            }
             int a = L - 1;
             for (; a >= 0; --a) {
                 if (++idx[a] < hi[a]) break;
@@ -497,7 +514,7 @@ int ctg_io_read_varlen(const char* ds_path, int dtype_size, int ndim, int64_t n_
             err.set("ctg_io_read_varlen: out of host memory");
             return;
         }
-        if (compression == CTG_IO_GZIP) {
+        if (compression != CTG_IO_RAW) {
             raw.resize((size_t)n * dtype_size);
             if (n && !inflate_all(payload, pn, raw.data(), raw.size())) {
                 free(dst);
@@ -527,6 +544,10 @@ int ctg_io_read_varlen(const char* ds_path, int dtype_size, int ndim, int64_t n_
 }
 
 void ctg_io_free(void* p) { free(p); }
+
+void ctg_io_cache_drop(const char* chunk_path) {
+    if (chunk_path) cache_drop(chunk_path);
+}
 
 void ctg_io_cache_clear(void) {
     std::lock_guard<std::mutex> g(g_cache_mu);
@@ -563,8 +584,8 @@ int ctg_io_write_chunks(const char* ds_path, int format, int dtype_size, int big
             for (int a = ndim - 1; a >= 0; --a) put_be32(hdr, (uint32_t)cs[a]);
             if (varlen) put_be32(hdr, (uint32_t)n);
         }
-        if (compression == CTG_IO_GZIP) {
-            if (!deflate_all(be.data(), be.size(), level < 0 ? 5 : level, true, payload)) {
+        if (compression != CTG_IO_RAW) {   // the stream type the dataset's metadata names
+            if (!deflate_all(be.data(), be.size(), level < 0 ? 5 : level, compression == CTG_IO_GZIP, payload)) {
                 err.set("ctg_io_write_chunks: deflate failed");
                 return;
             }

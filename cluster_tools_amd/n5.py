@@ -143,6 +143,20 @@ def _native():
     return _NATIVE or None
 
 
+def _replace_file(path, buf):
+    """Atomic chunk write (tmp file + rename), then drop the native codec's
+    cached decode of that chunk (ctg_io_read_box would otherwise keep serving
+    it if the rewrite kept size and mtime)."""
+    os.makedirs(os.path.dirname(path), exist_ok=True)
+    tmp = path + '.tmp%d_%d' % (os.getpid(), threading.get_ident())
+    with open(tmp, 'wb') as f:
+        f.write(buf)
+    os.replace(tmp, path)
+    lib = _native()
+    if lib is not None:
+        lib.ctg_io_cache_drop(path.encode())
+
+
 def _io_threads(n_threads):
     return max(1, int(n_threads) if n_threads and n_threads > 1 else min(16, os.cpu_count() or 1))
 
@@ -202,8 +216,12 @@ class Dataset:
         return 1
 
     def _ctype(self):
+        """CTG_IO_RAW / CTG_IO_GZIP / CTG_IO_ZLIB (N5 gzip with "useZlib": zlib
+        streams), None for codecs the native path lacks."""
         c = self.compression.get('type', 'raw')
-        return {'raw': 0, 'gzip': 1}.get(c)
+        if c == 'gzip':
+            return 2 if self.compression.get('useZlib', False) else 1
+        return {'raw': 0}.get(c)
 
     def _level(self):
         lv = self.compression.get('level', 5)
@@ -224,10 +242,15 @@ class Dataset:
         elif tuple(out.shape) != shape or out.dtype != self.dtype.newbyteorder('=') or not out.flags.c_contiguous:
             raise ValueError('read_box_native: out must be a C-contiguous %s array of shape %s'
                              % (self.dtype, shape))
+        fv = getattr(self, 'fill_value', 0)
+        fill = None
+        if fv:   # missing chunks read as the array's fill value (zarr), else zeros
+            fill = np.array([fv], dtype=self.dtype.newbyteorder('='))
         rc = lib.ctg_io_read_box(self.path.encode(), self._FORMAT, self.dtype.itemsize, self._big_endian(),
                                  self.ndim, _i64(self.shape), _i64(self.chunks), ct, _i64([b for b, _ in bb]),
                                  _i64([e for _, e in bb]), out.ctypes.data_as(ctypes.c_void_p),
-                                 _io_threads(n_threads or self.n_threads))
+                                 _io_threads(n_threads or self.n_threads),
+                                 None if fill is None else fill.ctypes.data_as(ctypes.c_void_p))
         if rc != 0:
             msg = lib.ctg_last_error()
             raise OSError(msg.decode() if msg else 'ctg_io_read_box failed')
@@ -237,7 +260,8 @@ class Dataset:
         """Write many chunks at once (native thread pool when available).
         Default-mode chunks must have their grid cell's shape."""
         positions = [tuple(int(p) for p in pos) for pos in positions]
-        datas = [np.ascontiguousarray(np.asarray(d, dtype=self.dtype)) for d in datas]
+        # native byte order: the codec swaps to the stored order itself (_big_endian)
+        datas = [np.ascontiguousarray(np.asarray(d, dtype=self.dtype.newbyteorder('='))) for d in datas]
         lib = _native()
         ct = self._ctype()
         if lib is None or ct is None or not positions:
@@ -321,12 +345,7 @@ class Dataset:
         else:
             shape = data.shape
             buf = self._encode(data, False, shape)
-        p = self._chunk_path(pos)
-        os.makedirs(os.path.dirname(p), exist_ok=True)
-        tmp = p + '.tmp%d_%d' % (os.getpid(), threading.get_ident())
-        with open(tmp, 'wb') as f:
-            f.write(buf)
-        os.replace(tmp, p)
+        _replace_file(self._chunk_path(pos), buf)
 
     def _read_multiset_chunk(self, pos):
         """argmax labels of a label-multiset chunk, or None if missing.
@@ -517,7 +536,8 @@ class ZarrArray(Dataset):
         c = self.compressor
         if c is None:
             return 0
-        return 1 if c.get('id') in _ZARR_CODECS else None   # other codecs: the Python path raises
+        # CTG_IO_GZIP / CTG_IO_ZLIB; other codecs: the Python path raises
+        return {'gzip': 1, 'zlib': 2}.get(c.get('id'))
 
     def _level(self):
         lv = (self.compressor or {}).get('level', 5)
@@ -562,12 +582,7 @@ class ZarrArray(Dataset):
             raw = co.compress(raw) + co.flush()
         elif cid == 'zlib':
             raw = zlib.compress(raw, level)
-        p = self._chunk_path(pos)
-        os.makedirs(os.path.dirname(p), exist_ok=True)
-        tmp = p + '.tmp%d_%d' % (os.getpid(), threading.get_ident())
-        with open(tmp, 'wb') as f:
-            f.write(raw)
-        os.replace(tmp, p)
+        _replace_file(self._chunk_path(pos), raw)
 
     def read_chunk(self, pos):
         p = self._chunk_path(pos)

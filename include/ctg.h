@@ -217,17 +217,22 @@ int ctg_synth_affinities(const float* boundary, float* affs, const int64_t* shap
  * features/block_edge_features.py:63-64, 236).
  *   format       CTG_IO_N5 | CTG_IO_ZARR_DOT (i.j.k keys) | CTG_IO_ZARR_SLASH
  *   big_endian   1: stored elements are big-endian (N5; zarr '>' dtypes)
- *   compression  CTG_IO_RAW | CTG_IO_GZIP (gzip or zlib streams on read)
+ *   compression  CTG_IO_RAW | CTG_IO_GZIP (writes gzip streams: N5 {"type":"gzip"},
+ *                zarr "gzip") | CTG_IO_ZLIB (writes zlib streams: N5 "useZlib":
+ *                true, zarr "zlib"); reads auto-detect gzip and zlib for both
  */
 #define CTG_IO_N5 0
 #define CTG_IO_ZARR_DOT 1
 #define CTG_IO_ZARR_SLASH 2
 #define CTG_IO_RAW 0
 #define CTG_IO_GZIP 1
-/* C-order box [begin, end) of a chunked dataset into `out` (missing chunks = 0) */
+#define CTG_IO_ZLIB 2
+/* C-order box [begin, end) of a chunked dataset into `out`; missing chunks are
+ * filled with the dtype_size-byte pattern fill_value (native byte order), or
+ * zeros when fill_value is NULL */
 int ctg_io_read_box(const char* ds_path, int format, int dtype_size, int big_endian, int ndim, const int64_t* shape,
                     const int64_t* chunks, int compression, const int64_t* begin, const int64_t* end, void* out,
-                    int n_threads);
+                    int n_threads, const void* fill_value);
 /* varlength N5 chunks at n_chunks grid positions: out[i] = malloc'ed native-
  * endian elements (free with ctg_io_free), n_out[i] = count, or NULL / -1 if
  * the chunk does not exist */
@@ -235,8 +240,11 @@ int ctg_io_read_varlen(const char* ds_path, int dtype_size, int ndim, int64_t n_
                        int compression, void** out, int64_t* n_out, int n_threads);
 void ctg_io_free(void* p);
 /* drop the decoded-chunk cache of ctg_io_read_box (budget: env CTG_IO_CACHE_MB,
- * default 4096; an entry is reused only while its file is unchanged) */
+ * default 4096; an entry is reused only while its file keeps its inode, size,
+ * mtime and ctime -- every writer here replaces chunk files by rename) */
 void ctg_io_cache_clear(void);
+/* drop the cached decodes of one chunk file (writers outside ctg_io call it) */
+void ctg_io_cache_drop(const char* chunk_path);
 /* write n_chunks chunks (default mode with chunk_shapes, or N5 varlength) */
 int ctg_io_write_chunks(const char* ds_path, int format, int dtype_size, int big_endian, int ndim, int64_t n_chunks,
                         const int64_t* positions, const int64_t* chunk_shapes, const void* const* data,

@@ -68,6 +68,29 @@ def test_blocks_graph_matches_per_block_oracle(gpu, ignore_label, label_shift):
         np.testing.assert_array_equal(r['edges'], O.rag_edges(lab[g['outer']], ignore_label=ignore_label))
 
 
+def test_blocks_ignore_label_dense_relabel_without_zero(gpu):
+    """ignore_label=True, no label 0 anywhere, labels above the block tag's
+    range (2^(32 - tag_bits)) and above 2^32: the batched call relabels the
+    arena densely; the smallest real label must not become the ignore label
+    (its edges would be dropped).  Same for the whole-volume call."""
+    shape, block = (26, 41, 70), (8, 16, 32)
+    lab, bnd = S.generate(shape, cell=5, seed=45)
+    for shift in (np.uint64(1) << np.uint64(29), np.uint64(1) << np.uint64(40)):
+        big = lab + shift                           # no zeros
+        geo = _block_geometry(shape, block)
+        res = rag.rag_blocks([big[g['roi']] for g in geo], [g['own'] for g in geo], [g['graph'] for g in geo],
+                             data=[bnd[g['roi']] for g in geo], ignore_label=True)
+        for g, r in zip(geo, res):
+            np.testing.assert_array_equal(r['nodes'], np.unique(big[g['inner']]))
+            eb, f = _expected_boundary(big, bnd, g, ignore_label=True)
+            np.testing.assert_array_equal(r['edges'], eb)
+            check_features(r['features'], f)
+        out = rag.rag_features(big, bnd, ignore_label=True)
+        e_ref, f_ref = O.boundary_features(big, bnd, ignore_label=True)
+        np.testing.assert_array_equal(out['edges'], e_ref)
+        check_features(out['features'], f_ref)
+
+
 @pytest.mark.parametrize('dtype', ['float32', 'uint8'])
 def test_blocks_boundary_features(gpu, dtype):
     shape, block = (30, 37, 66), (10, 16, 32)

@@ -384,6 +384,82 @@ def test_native_chunk_cache_sees_rewrites_and_threads(tmp_path, monkeypatch):
     n5._native().ctg_io_cache_clear()
 
 
+def test_native_writer_follows_the_declared_stream_type(tmp_path, monkeypatch):
+    """N5 gzip with "useZlib": true and zarr "zlib" get zlib streams from the
+    native writer (plain zlib.decompress reads them), N5 / zarr "gzip" get gzip
+    streams (magic 1f 8b), as numcodecs / z5 readers of that metadata expect."""
+    import json
+    import zlib
+    _with_codec(monkeypatch, True)
+    data = np.arange(4 * 8 * 8, dtype=np.uint64).reshape(4, 8, 8)
+    cases = [('n5', {'type': 'gzip', 'level': 3, 'useZlib': True}, 'zlib'),
+             ('n5', {'type': 'gzip', 'level': 3, 'useZlib': False}, 'gzip'),
+             ('zarr', {'type': 'gzip', 'level': 3, 'useZlib': True}, 'zlib'),
+             ('zarr', {'type': 'gzip', 'level': 3, 'useZlib': False}, 'gzip')]
+    for i, (ext, comp, stream) in enumerate(cases):
+        p = str(tmp_path / ('s%d.%s' % (i, ext)))
+        with n5.file_reader(p) as f:
+            ds = f.create_dataset('d', shape=data.shape, chunks=(4, 8, 8), dtype='uint64', compression=comp)
+            ds[:] = data                                    # aligned: the native batched writer
+        if ext == 'n5':
+            with open(os.path.join(p, 'd', '0', '0', '0'), 'rb') as fh:
+                buf = fh.read()[4 + 4 * 3:]
+            raw_dt = '>u8'
+        else:
+            assert json.load(open(os.path.join(p, 'd', '.zarray')))['compressor']['id'] == stream
+            with open(os.path.join(p, 'd', '0.0.0'), 'rb') as fh:
+                buf = fh.read()
+            raw_dt = '<u8'
+        if stream == 'zlib':
+            raw = zlib.decompress(buf)
+        else:
+            assert buf[:2] == b'\x1f\x8b'
+            raw = zlib.decompress(buf, 16 + zlib.MAX_WBITS)
+        np.testing.assert_array_equal(np.frombuffer(raw, dtype=raw_dt).reshape(data.shape), data)
+
+
+def test_native_cache_sees_same_size_raw_rewrite(tmp_path, monkeypatch):
+    """Uncompressed chunks keep their size on rewrite and a quick rewrite may
+    keep the mtime: the decoded-chunk cache keys on the inode (rewrites are
+    renames) and the Python writer drops the entry."""
+    _with_codec(monkeypatch, True)
+    p = str(tmp_path / 'r.n5')
+    data = np.arange(8 * 8 * 8, dtype=np.uint32).reshape(8, 8, 8)
+    with n5.File(p) as f:
+        ds = f.create_dataset('d', shape=data.shape, chunks=(8, 8, 8), dtype='uint32', compression='raw')
+        ds[:] = data
+        for k in range(1, 6):
+            np.testing.assert_array_equal(ds[:], data + k - 1)
+            ds.write_chunk((0, 0, 0), data + k)             # python writer, same size
+        np.testing.assert_array_equal(ds[:], data + 5)
+    n5._native().ctg_io_cache_clear()
+
+
+def test_zarr_fill_value_and_big_endian(tmp_path, monkeypatch):
+    """zarr: missing chunks read as the array's fill_value on both codecs;
+    a '>u8' array written by the native writer lands big-endian on disk."""
+    import json
+    for native in (True, False):
+        _with_codec(monkeypatch, native)
+        p = str(tmp_path / ('z%d.zarr' % native))
+        data = np.arange(6 * 8 * 10, dtype=np.uint64).reshape(6, 8, 10) * np.uint64(1 << 33)
+        with n5.file_reader(p) as f:
+            f.create_dataset('d', shape=data.shape, chunks=(3, 8, 5), dtype='>u8', compression='raw')
+        meta_p = os.path.join(p, 'd', '.zarray')
+        meta = json.load(open(meta_p))
+        meta['fill_value'] = 7
+        json.dump(meta, open(meta_p, 'w'))
+        with n5.file_reader(p) as f:
+            ds = f['d']
+            ds[:3] = data[:3]                               # chunks (1, *, *) stay missing
+            got = ds[:]
+            np.testing.assert_array_equal(got[:3], data[:3])
+            assert np.all(got[3:] == 7)
+        with open(os.path.join(p, 'd', '0.0.0'), 'rb') as fh:
+            raw = np.frombuffer(fh.read(), dtype='>u8').reshape(3, 8, 5)
+        np.testing.assert_array_equal(raw, data[:3, :, :5])
+
+
 def serialize_argmax_multiset(labels):
     """A label multiset of one label per voxel in the imglib2 / paintera N5
     serialisation (test-side writer, the restated format of n5.Dataset.
