@@ -47,7 +47,14 @@ enum { MODE_GRAPH = 0, MODE_BOUNDARY = 1, MODE_AFFINITY = 2 };
 // (the workgroup's tile cross-section, hence its live edge set, halves: the
 // table then holds it and flushes -- records -- drop by ~40 % at cell 5)
 constexpr int ROWS_WIDE = CTG_ROWS;
-constexpr int ROWS_NARROW = 2;
+#ifndef CTG_ROWS_NARROW
+#define CTG_ROWS_NARROW 2
+#endif
+constexpr int ROWS_NARROW = CTG_ROWS_NARROW;
+#ifndef CTG_AFF_ROWS
+#define CTG_AFF_ROWS CTG_ROWS
+#endif
+constexpr int ROWS_AFF = CTG_AFF_ROWS;   // affinity maps: rows per wave (the channel loop's registers scale with it)
 constexpr int WAVES = SCAN_THREADS / WAVE;                // 8
 constexpr int WG_ROWS = ROWS_WIDE * WAVES;                // tile y extent (the default kernel)
 #ifndef CTG_AFF_G
@@ -300,19 +307,49 @@ __device__ __forceinline__ void hist_add2(Table& T, int e, int sa, int sb) {
 // took the table past FILL_SOFT (a flag, not a reference: a bool& argument of
 // an out-of-line call would live in scratch memory).
 constexpr int INSERT_OVER = 0x10000;
+#ifndef CTG_PROBE_BUCKETS
+#define CTG_PROBE_BUCKETS 16   // buckets (of 4 slots) a key may walk past its home bucket
+#endif
 __device__ __noinline__ int table_insert(Table& T, uint32_t h, int empty, uint64_t key) {
-    // probe order is linear from the bucket start, so the key cannot sit
-    // beyond an empty slot; a lost race or a full bucket walks on
-    uint32_t p = h + (empty >= 0 ? (uint32_t)empty : 4u);
+    // Probe order is linear from the home bucket's start, so a key never sits
+    // beyond an empty slot; a lost race or a full bucket walks on.  Whole
+    // buckets are read at a time (two ds_read_b128, as the home-bucket probe):
+    // one LDS round trip per 4 slots instead of one per slot.
+    uint32_t b = h;
+    int j0 = empty >= 0 ? empty : 4;   // first slot of bucket b still to look at
 #pragma unroll 1
-    for (int i = 0; i < 64; ++i, p = (p + 1) & (TABLE_CAP - 1)) {
-        const uint64_t cur = __hip_atomic_load(&T.key[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        if (cur == key) return (int)p;
-        if (cur != EMPTY_KEY) continue;
-        const uint64_t old =
-            atomicCAS((unsigned long long*)&T.key[p], (unsigned long long)EMPTY_KEY, (unsigned long long)key);
-        if (old == EMPTY_KEY) return (int)p | (atomicAdd(&T.used, 1u) + 1u > FILL_SOFT ? INSERT_OVER : 0);
-        if (old == key) return (int)p;
+    for (int i = 0; i <= CTG_PROBE_BUCKETS;) {
+        if (j0 >= 4) {
+            b = (b + 4) & (TABLE_CAP - 1);
+            j0 = 0;
+            ++i;
+            continue;
+        }
+        const uint4 b01 = *reinterpret_cast<const uint4*>(&T.key[b]);
+        const uint4 b23 = *reinterpret_cast<const uint4*>(&T.key[b + 2]);
+        const uint64_t kk[4] = {((uint64_t)b01.y << 32) | b01.x, ((uint64_t)b01.w << 32) | b01.z,
+                                ((uint64_t)b23.y << 32) | b23.x, ((uint64_t)b23.w << 32) | b23.z};
+        uint32_t km = 0, em = 0;   // slots (>= j0) holding the key / empty, as bit masks
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            km |= (kk[j] == key ? 1u : 0u) << j;
+            em |= (kk[j] == EMPTY_KEY ? 1u : 0u) << j;
+        }
+        const uint32_t live = ~((1u << j0) - 1u);
+        km &= live;
+        em &= live;
+        if ((km | em) == 0) {
+            j0 = 4;
+            continue;
+        }
+        const int first = __builtin_ctz(km | em);
+        if ((km >> first) & 1u) return (int)(b + first);
+        const uint64_t old = atomicCAS((unsigned long long*)&T.key[b + first], (unsigned long long)EMPTY_KEY,
+                                       (unsigned long long)key);
+        if (old == EMPTY_KEY)
+            return (int)(b + first) | (atomicAdd(&T.used, 1u) + 1u > FILL_SOFT ? INSERT_OVER : 0);
+        if (old == key) return (int)(b + first);
+        j0 = first + 1;   // lost the slot to another key: re-read the rest of the bucket
     }
     return -1;
 }
@@ -456,7 +493,7 @@ __device__ __forceinline__ void fold_batch(Table& T, const StageT* __restrict__ 
                 }
             }
         }
-        slot[i] = s;
+        slot[i] = valid ? s : -2;   // -2: nothing to fold
     }
     // the entries' pivot words, read together (one LDS round trip for the batch)
     uint32_t pv[NPER];
@@ -468,7 +505,7 @@ __device__ __forceinline__ void fold_batch(Table& T, const StageT* __restrict__ 
     }
 #pragma unroll
     for (int i = 0; i < NPER; ++i)
-        if (lane + WAVE * i < nb)
+        if (slot[i] != -2)
             fold_stats<MODE, FAST40, BATCH, StageT>(T, e[i], slot[i], pv[i], R, C, scale, offset, need, ablate);
 }
 
@@ -984,6 +1021,9 @@ static hipError_t launch_scan_t(const ScanParams& P, const RecordBuf& R, Counter
         }
         if (P.narrow_rows == 1 && !P.blocks) return launch_scan_r<LabelT, DataT, MODE, ROWS_NARROW>(P, R, C, s);
     }
+    // (batched blocks keep the wide tile: their tile counts come from scan_tile_rows())
+    if constexpr (MODE == MODE_AFFINITY)
+        if (!P.blocks) return launch_scan_r<LabelT, DataT, MODE, ROWS_AFF>(P, R, C, s);
     return launch_scan_r<LabelT, DataT, MODE, ROWS_WIDE>(P, R, C, s);
 }
 
