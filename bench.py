@@ -229,6 +229,7 @@ def bench_config0(args):
     ms = float(np.mean(times)) * 1e3
     scan_avg = float(np.mean(scan_ms))
     alg = lo * 12                                   # the feature scan reads every block array (+ halo) once
+    traffic, traffic_src = pmc_traffic_per_launch('0') if not args.cell else (None, None)
     line = {
         'metric': 'Gvoxels/s RAG+edge features (per-block drop-in path, gzip N5 in -> N5 out, uint64 labels, '
                   'float32 boundary map)',
@@ -251,7 +252,8 @@ def bench_config0(args):
         'roofline': {'bound': 'hbm', 'kernel': 'k_face_scan (batched blocks, features)',
                      'kernel_ms': round(scan_avg, 4), 'algorithmic_bytes': alg,
                      'achieved': round(alg / (scan_avg * 1e-3) / 1e9, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
-                     'frac': round(alg / (scan_avg * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), 'traffic': None},
+                     'frac': round(alg / (scan_avg * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), 'traffic': traffic,
+                     'traffic_source': traffic_src},
         'cpu_baseline': None,
     }
     print(json.dumps(line), flush=True)

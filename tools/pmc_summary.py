@@ -1,6 +1,6 @@
 """Summarise rocprofv3 CSV output into profiles/<round>/*.json.
 
-usage: python tools/pmc_summary.py <trace_dir> <pmc_dir_fetch> <pmc_dir_write> <out.json> [algorithmic_bytes]
+usage: python tools/pmc_summary.py <trace_dir> <pmc_dir_fetch> <pmc_dir_write> <out.json> [algorithmic_bytes [git_sha]]
 
 * kernel stats: <trace_dir>/**/*kernel_stats.csv (Name, Calls, AverageNs ...)
 * PMC: <pmc_dir>/**/*counter_collection.csv, one row per (dispatch, counter)
@@ -54,6 +54,7 @@ def pick(d, sub):
 def main():
     trace, pf, pw, out = sys.argv[1:5]
     alg = float(sys.argv[5]) if len(sys.argv) > 5 else None
+    sha = sys.argv[6] if len(sys.argv) > 6 else None
     stats = kernel_stats(trace)
     fetch = counter_per_dispatch(pf, 'FETCH_SIZE')
     write = counter_per_dispatch(pw, 'WRITE_SIZE')
@@ -65,7 +66,17 @@ def main():
         'write_size_kib_per_dispatch': write,
         'read_factor': 2.0,
         'note': 'HBM bytes = 2 x FETCH_SIZE x 1024 + WRITE_SIZE x 1024 (gfx950 FETCH_SIZE halving)',
+        'git_sha': sha,
     }
+    # the face scan's average duration from the kernel trace (the launched
+    # variant: the unselected tile width exits at once and has a tiny average)
+    scans = {k: v for k, v in stats.items() if 'k_face_scan' in k}
+    if scans:
+        name, st = max(scans.items(), key=lambda kv: kv[1]['avg_ns'])
+        summary['scan_kernel'] = name
+        summary['scan_avg_ns'] = st['avg_ns']
+        if alg:
+            summary['scan_frac_from_stats'] = alg / (st['avg_ns'] * 1e-9) / 8.0e12
     if scan_f is not None and scan_w is not None:
         summary['scan_hbm_bytes_per_launch'] = 2.0 * scan_f * 1024 + scan_w * 1024
         summary['scan_read_bytes_per_launch'] = 2.0 * scan_f * 1024

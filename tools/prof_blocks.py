@@ -28,6 +28,9 @@ for b in range(blk.numberOfBlocks):
 la = torch.cat([lt[s].reshape(-1) for s in sls])
 da = torch.cat([bt[s].reshape(-1) for s in sls])
 del lt, bt
+# algorithmic bytes of the feature call's face scan: every block array (+ halo)
+# read once, 8 B label + 4 B sample per voxel (bench.py --config 0)
+print('feature_scan_bytes=%d' % (lo * 12), flush=True)
 rag.set_profiling(True)
 for i in range(int(os.environ.get('CTG_PROF_ITERS', '4'))):
     torch.cuda.synchronize()
