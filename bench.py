@@ -16,10 +16,11 @@ them over RCCL (cluster_tools_amd/dist.py).
 The other BASELINE configs are extra lines (``--config``), not the driver's
 bench line:
   0    configs[0]: the drop-in per-block path end to end -- GraphWorkflow +
-       EdgeFeaturesWorkflow job bodies (cluster_tools_amd/workflow.py) on a
+       EdgeFeaturesWorkflow job bodies (harness/workflow.py) on a
        125 x 1250 x 1250 volume in gzip N5 with 64 x 256 x 256 blocks, N5 in ->
-       N5 out; value = end-to-end Gvoxels/s, plus the compute-only rate of the
-       same per-block calls on device-resident inputs and the stage split
+       N5 out; value = end-to-end Gvoxels/s with every job its own process
+       (the reference's LocalTask model), plus the same with job threads and
+       the compute-only rate of the per-block calls on device-resident inputs
   2    configs[2]: 2048^3 boundary map (cell 16), strong scaling: the fixed
        volume is z-sharded over the ranks (2048/N planes each + 1 halo plane)
   3    configs[3]: 1024^3, 3-channel nearest-neighbour affinities (N=1)
@@ -139,36 +140,59 @@ def cpu_baseline(labels_t, bnd_t, planes, workers):
         seconds=best, threads=workers)
 
 
-def bench_config0(args):
-    """BASELINE configs[0]: the per-block drop-in path, N5 in -> N5 out."""
-    import shutil
-    import tempfile
-    import torch
-    from cluster_tools_amd import _lib, n5, rag, workflow
-    from cluster_tools_amd.blocking import blocking
-    _lib.init_device(0 if args.device is None else args.device)
-    shape, block = (125, 1250, 1250), (64, 256, 256)
-    V = int(np.prod(shape))
-    lt, bt = rag.synth_volume(shape, cell=args.cell or 10, seed=args.seed)
+def _config0_write_inputs(path, shape, block, cell, seed):
+    """configs[0] input: the synthetic volume generated on the GPU and written
+    as gzip N5 (level 1) -- in a child process, so the bench process itself
+    has not touched the device when the process-mode jobs start (the GPU box
+    allows 16 processes on the card)."""
+    from cluster_tools_amd import _lib, n5, rag
+    _lib.init_device(0)
+    lt, bt = rag.synth_volume(shape, cell=cell, seed=seed)
     lab = lt.cpu().numpy().view(np.uint64)
     bnd = bt.cpu().numpy()
+    comp = {'type': 'gzip', 'level': 1, 'useZlib': False}
+    with n5.File(path) as f:
+        for key, arr in (('seg', lab), ('bnd', bnd)):
+            ds = f.create_dataset(key, shape=shape, chunks=block, dtype=arr.dtype, compression=comp)
+            ds.n_threads = 16
+            ds[:] = arr
+    return sum(os.path.getsize(os.path.join(r, fn)) for r, _, fs in os.walk(path) for fn in fs)
+
+
+# job processes of the process-mode graph task: the GPU box allows 16
+# processes on the card, and the bench process joins them in thread mode
+CONFIG0_PROC_JOBS = 15
+
+
+def bench_config0(args):
+    """BASELINE configs[0]: the per-block drop-in path, N5 in -> N5 out.
+
+    Two job models over the same N5 input: ``processes`` (the reference's --
+    LocalTask runs every job as its own process, cluster_tasks.py:528-550;
+    this is ``value``) and ``threads`` (every job on a thread of this process,
+    sharing the device state and the decoded-chunk cache), then the
+    device-only time of the same per-block calls."""
+    import multiprocessing as mp
+    import shutil
+    import tempfile
+    from concurrent.futures import ProcessPoolExecutor
+    from harness import workflow
+    shape, block = (125, 1250, 1250), (64, 256, 256)
+    V = int(np.prod(shape))
+    cell = args.cell or 10
     tmp_root = '/dev/shm' if os.path.isdir('/dev/shm') and shutil.disk_usage('/dev/shm').free > 12e9 else None
     d = tempfile.mkdtemp(prefix='ctg_cfg0_', dir=tmp_root)
     try:
         inp = os.path.join(d, 'in.n5')
-        comp = {'type': 'gzip', 'level': 1, 'useZlib': False}
-        with n5.File(inp) as f:
-            for key, arr in (('seg', lab), ('bnd', bnd)):
-                ds = f.create_dataset(key, shape=shape, chunks=block, dtype=arr.dtype, compression=comp)
-                ds.n_threads = 16
-                ds[:] = arr
-        in_bytes = sum(os.path.getsize(os.path.join(r, fn)) for r, _, fs in os.walk(inp) for fn in fs)
+        with ProcessPoolExecutor(1, mp_context=mp.get_context('spawn')) as ex:
+            in_bytes = ex.submit(_config0_write_inputs, inp, shape, block, cell, args.seed).result()
 
-        def step(k):
+        def step(k, mode, graph_jobs):
             out = os.path.join(d, 'out%d.n5' % k)
-            t = workflow.graph_workflow(inp, 'seg', out, 'graph', block, max_jobs=16)
+            t = workflow.graph_workflow(inp, 'seg', out, 'graph', block, max_jobs=graph_jobs, mode=mode)
             workflow.edge_features_workflow(inp, 'bnd', inp, 'seg', out, 'graph', out, 'features', block,
-                                            max_jobs=1, max_jobs_merge=4, timer=t)
+                                            max_jobs=1, max_jobs_merge=4, timer=t, mode=mode)
+            from cluster_tools_amd import n5
             with n5.File(out, 'r') as f:
                 n_edges = int(f['graph'].attrs['numberOfEdges'])
             shutil.rmtree(out)
@@ -176,18 +200,34 @@ def bench_config0(args):
 
         # a step is a whole workflow run (seconds): at most 1 warm-up + 3 steps
         args.warmup, args.steps = min(args.warmup, 1), max(1, min(args.steps, 3))
-        for k in range(args.warmup):
-            step(k)
-        times, stages, feat_prof = [], {}, {}
-        from cluster_tools_amd import ndist
-        for k in range(args.steps):
-            t0 = time.perf_counter()
-            st, n_edges = step(100 + k)
-            times.append(time.perf_counter() - t0)
-            for key, v in st.items():
-                stages[key] = stages.get(key, 0.0) + v / args.steps
-            for key, v in ndist.last_profile.items():   # the (single) block-feature job's split
-                feat_prof[key] = feat_prof.get(key, 0.0) + v / args.steps
+
+        def measure(mode, graph_jobs, base):
+            for k in range(args.warmup):
+                step(base + k, mode, graph_jobs)
+            times, stages, feat_prof = [], {}, {}
+            from cluster_tools_amd import ndist
+            for k in range(args.steps):
+                t0 = time.perf_counter()
+                st, n_edges = step(base + 100 + k, mode, graph_jobs)
+                times.append(time.perf_counter() - t0)
+                for key, v in st.items():
+                    stages[key] = stages.get(key, 0.0) + v / args.steps
+                if mode == 'threads':   # the (single) block-feature job's split, in this process
+                    for key, v in ndist.last_profile.items():
+                        feat_prof[key] = feat_prof.get(key, 0.0) + v / args.steps
+            return float(np.mean(times)) * 1e3, stages, feat_prof, n_edges
+
+        # process mode first: this process has not opened the device yet
+        ms_p, stages_p, _, n_edges = measure('processes', CONFIG0_PROC_JOBS, 0)
+        ms_t, stages_t, feat_prof, _ = measure('threads', 16, 1000)
+
+        import torch
+        from cluster_tools_amd import _lib, n5, rag
+        from cluster_tools_amd.blocking import blocking
+        _lib.init_device(0 if args.device is None else args.device)
+        with n5.File(inp, 'r') as f:
+            lt = torch.from_numpy(f['seg'][:].view(np.int64)).cuda()
+            bt = torch.from_numpy(f['bnd'][:]).cuda()
         # compute only: the same per-block calls on device-resident inputs
         blk = blocking([0, 0, 0], list(shape), list(block))
         descs, lo = [], 0
@@ -226,23 +266,28 @@ def bench_config0(args):
         rag.set_profiling(False)
     finally:
         shutil.rmtree(d, ignore_errors=True)
-    ms = float(np.mean(times)) * 1e3
     scan_avg = float(np.mean(scan_ms))
     alg = lo * 12                                   # the feature scan reads every block array (+ halo) once
     traffic, traffic_src = pmc_traffic_per_launch('0') if not args.cell else (None, None)
     line = {
         'metric': 'Gvoxels/s RAG+edge features (per-block drop-in path, gzip N5 in -> N5 out, uint64 labels, '
                   'float32 boundary map)',
-        'value': round(V / (ms * 1e-3) / 1e9, 4), 'unit': 'Gvoxels/s', 'n_gpus': 1, 'steps': args.steps,
-        'warmup': args.warmup, 'ms_per_step': round(ms, 2), 'higher_is_better': True, 'scaling': 'weak',
+        'value': round(V / (ms_p * 1e-3) / 1e9, 4), 'unit': 'Gvoxels/s', 'n_gpus': 1, 'steps': args.steps,
+        'warmup': args.warmup, 'ms_per_step': round(ms_p, 2), 'higher_is_better': True, 'scaling': 'weak',
         'vs_baseline': None, 'dtype': 'u64 labels / f32 samples / f64 stats',
         'data': 'synthetic (jittered-grid Voronoi supervoxels + boundary map) written to gzip N5 (level 1)',
         'config': {'workload': 'BASELINE configs[0]: 125x1250x1250, 64x256x256 blocks (50), GraphWorkflow + '
-                               'EdgeFeaturesWorkflow job bodies (16 graph jobs, 1 feature job, 4 merge jobs)',
+                               'EdgeFeaturesWorkflow job bodies (harness/workflow.py), every job its own spawned '
+                               'process as LocalTask runs them (%d graph jobs, 1 feature job, 4 merge jobs)'
+                               % CONFIG0_PROC_JOBS,
                    'volume': list(shape), 'block_shape': list(block), 'edges': n_edges,
                    'input_n5_bytes': in_bytes},
-        'stage_s': {k: round(v, 4) for k, v in stages.items()},
-        'block_features_split_s': {k: round(v, 4) for k, v in feat_prof.items()},
+        'stage_s': {k: round(v, 4) for k, v in stages_p.items()},
+        'thread_mode': {'value': round(V / (ms_t * 1e-3) / 1e9, 4), 'unit': 'Gvoxels/s', 'ms_per_step': round(ms_t, 2),
+                        'stage_s': {k: round(v, 4) for k, v in stages_t.items()},
+                        'block_features_split_s': {k: round(v, 4) for k, v in feat_prof.items()},
+                        'what': 'the same workflow with every job on a thread of the bench process (16 graph jobs; '
+                                'jobs share the device state and the decoded-chunk cache)'},
         'compute_only': {'value': round(V / compute_s / 1e9, 4), 'unit': 'Gvoxels/s',
                          'ms': round(compute_s * 1e3, 3),
                          'with_d2h_ms': round(wall_s * 1e3, 3),

@@ -8,6 +8,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import sys
 import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -146,11 +147,14 @@ def init_device(device=None):
     or 0) and create the per-device workspace."""
     lib = load()
     if device is None:
-        try:
-            import torch
-            device = torch.cuda.current_device() if torch.cuda.is_available() else 0
-        except Exception:  # pragma: no cover - torch always present in this image
-            device = 0
+        # torch's current device when the caller already uses torch on the GPU;
+        # otherwise CTG_DEVICE (default 0) -- a job process of the drop-in path
+        # never imports torch (its import and runtime start cost seconds)
+        torch = sys.modules.get('torch')
+        if torch is not None and torch.cuda.is_initialized():
+            device = torch.cuda.current_device()
+        else:
+            device = int(os.environ.get('CTG_DEVICE', '0'))
     check(lib.ctg_init(int(device)), 'ctg_init(%d)' % device)
     _inited.add(int(device))
     return int(device)

@@ -1,0 +1,341 @@
+"""Test / bench harness: the hot path's two workflows without luigi.
+
+Not product code: the luigi task classes stay the reference's and call the
+mirrored ``ndist`` functions.  This module restates, for the
+end-to-end GPU tests and ``bench.py --config 0``, what those tasks do around
+the ``ndist`` calls: ``GraphWorkflow`` (graph/graph_workflow.py:22-66) and
+``EdgeFeaturesWorkflow`` (features/features_workflow.py:31-57) with
+``n_scales=1`` and ``target='local'``.  Every task's run_impl creates the
+datasets and attributes it creates, and its jobs -- ``block_list[k::n_jobs]``
+(cluster_tasks.py:301-335) -- run the job bodies (the ndist call sequence).
+
+    InitialSubGraphs   initial_sub_graphs.py:49-90, job :134-157
+    MergeSubGraphs     merge_sub_graphs.py:52-96, job :155-195 (complete graph)
+    MapEdgeIds         map_edge_ids.py:36-70, job :101-120
+    BlockEdgeFeatures  block_edge_features.py:48-87, job :275-327 (_accumulate, and the
+                       filter branch _accumulate_with_filters :151-272 on the GPU filters)
+    MergeEdgeFeatures  merge_edge_features.py:35-84, job :110-149
+
+Job execution (``mode``):
+  * ``'processes'`` -- the reference's process model: ``LocalTask._submit``
+    starts every job as its own process (``call([script, config])`` in a
+    ``ProcessPoolExecutor``, cluster_tasks.py:528-550); here every job is a
+    freshly spawned Python process that imports the library, opens the
+    device, runs its job body and exits.  Nothing is shared between jobs but
+    the files.
+  * ``'threads'`` -- every job on a thread of the calling process (job calls
+    share the library's device state and decoded-chunk caches).
+"""
+from __future__ import annotations
+
+import functools
+import multiprocessing as mp
+import time
+import traceback
+from concurrent.futures import ThreadPoolExecutor
+
+import numpy as np
+
+from cluster_tools_amd import fastfilters, ndist
+from cluster_tools_amd.blocking import blocking, blocks_in_volume
+
+
+def _jobs(block_list, n_jobs):
+    n_jobs = max(1, min(len(block_list), n_jobs))
+    return [block_list[k::n_jobs] for k in range(n_jobs)]
+
+
+def _proc_main(conn, fn, job):
+    """Body of a job process: run the job, send ('ok', result) or ('err', text)."""
+    try:
+        conn.send(('ok', fn(job)))
+    except BaseException:  # noqa: BLE001 -- reported to the parent, which raises
+        conn.send(('err', traceback.format_exc()))
+    finally:
+        conn.close()
+
+
+def _run_job_processes(fn, jobs):
+    """One spawned process per job, all of a task's jobs at once (the task's
+    max_jobs); results in job order.  A job that fails or dies fails the task
+    (LocalTask checks each job's log for success, cluster_tasks.py:575-590)."""
+    ctx = mp.get_context('spawn')
+    procs = []
+    try:
+        for j in jobs:
+            r, w = ctx.Pipe(duplex=False)
+            p = ctx.Process(target=_proc_main, args=(w, fn, j), daemon=True)
+            p.start()
+            w.close()
+            procs.append((p, r))
+        out, errors = [], []
+        for k, (p, r) in enumerate(procs):
+            try:
+                status, val = r.recv()
+            except EOFError:
+                status, val = 'err', 'job process exited without a result'
+            p.join()
+            if status == 'ok' and p.exitcode == 0:
+                out.append(val)
+            else:
+                errors.append('job %d (exit code %s): %s' % (k, p.exitcode, val))
+        if errors:
+            raise RuntimeError('task failed:\n' + '\n'.join(errors))
+        return out
+    finally:
+        for p, r in procs:
+            r.close()
+            if p.is_alive():
+                p.terminate()
+                p.join()
+
+
+def _run_jobs(fn, jobs, mode='threads'):
+    """Run the job bodies; their return values in job order."""
+    if mode == 'processes':
+        return _run_job_processes(fn, jobs)
+    if mode != 'threads':
+        raise ValueError('mode must be "threads" or "processes"')
+    if len(jobs) == 1:
+        return [fn(jobs[0])]
+    with ThreadPoolExecutor(len(jobs)) as ex:
+        return [f.result() for f in [ex.submit(fn, j) for j in jobs]]
+
+
+def _run_single(fn, mode):
+    """A task with one job (MergeSubGraphs / MapEdgeIds: max_jobs 1)."""
+    return _run_jobs(_call0, [fn], mode)[0]
+
+
+def _call0(fn):
+    return fn()
+
+
+class Timer:
+    def __init__(self):
+        self.stages = {}
+
+    def stage(self, name):
+        timer = self
+
+        class _Ctx:
+            def __enter__(self):
+                self.t = time.perf_counter()
+
+            def __exit__(self, *a):
+                timer.stages[name] = timer.stages.get(name, 0.0) + time.perf_counter() - self.t
+        return _Ctx()
+
+
+# ------------------------------------------------------------------ job bodies
+# (top-level functions with plain arguments: a spawned job process unpickles them)
+
+def _initial_sub_graphs_job(input_path, input_key, graph_path, shape, block_shape, ignore_label, blocks):
+    """initial_sub_graphs.py:134-157."""
+    blk = blocking([0, 0, 0], list(shape), list(block_shape))
+    for b in blocks:
+        block = blk.getBlock(b)
+        ndist.computeMergeableRegionGraph(input_path, input_key, block.begin, block.end, graph_path,
+                                          's0/sub_graphs', ignore_label, increaseRoi=True,
+                                          serializeToVarlen=True)
+
+
+def _merge_sub_graphs_job(graph_path, block_list, output_key, threads_per_job):
+    """merge_sub_graphs.py:130-137."""
+    ndist.mergeSubgraphs(graph_path, subgraphKey='s0/sub_graphs', blockIds=block_list, outKey=output_key,
+                         numberOfThreads=threads_per_job, serializeToVarlen=False)
+
+
+def _map_edge_ids_job(graph_path, output_key, block_list, threads_per_job):
+    """map_edge_ids.py:116-119."""
+    ndist.mapEdgeIds(graph_path, output_key, subgraphKey='s0/sub_graphs', blockIds=block_list,
+                     numberOfThreads=threads_per_job)
+
+
+def graph_workflow(input_path, input_key, graph_path, output_key, block_shape, max_jobs=16, threads_per_job=16,
+                   ignore_label=False, timer=None, mode='threads'):
+    """GraphWorkflow(n_scales=1): per-block sub-graphs, the merged graph at
+    ``output_key``, per-block edge ids."""
+    timer = timer or Timer()
+    with ndist._open(input_path, 'r') as f:
+        shape = list(f[input_key].shape)
+    block_list = blocks_in_volume(shape, block_shape)
+    with timer.stage('initial_sub_graphs'):
+        with ndist._open(graph_path) as f:                      # initial_sub_graphs.py:64-75
+            g = f.require_group('s0/sub_graphs')
+            g.attrs['shape'] = shape
+            g.attrs['ignore_label'] = bool(ignore_label)
+            for k in ('nodes', 'edges'):
+                g.require_dataset(k, shape=shape, chunks=list(block_shape), compression='gzip', dtype='uint64')
+        job = functools.partial(_initial_sub_graphs_job, input_path, input_key, graph_path, shape,
+                                list(block_shape), ignore_label)
+        _run_jobs(job, _jobs(block_list, max_jobs), mode)
+    with timer.stage('merge_sub_graphs'):
+        with ndist._open(graph_path) as f:                      # merge_sub_graphs.py:61-68
+            g = f.require_group(output_key)
+            g.attrs['ignore_label'] = bool(ignore_label)
+            g.attrs['shape'] = shape
+        _run_single(functools.partial(_merge_sub_graphs_job, graph_path, block_list, output_key, threads_per_job),
+                    mode)
+        with ndist._open(graph_path) as f:                      # merge_sub_graphs.py:136-137
+            f[output_key].attrs['shape'] = shape
+    with timer.stage('map_edge_ids'):
+        with ndist._open(graph_path) as f:                      # map_edge_ids.py:44-53
+            f.require_dataset('s0/sub_graphs/edge_ids', shape=shape, chunks=list(block_shape),
+                              compression='gzip', dtype='uint64')
+        _run_single(functools.partial(_map_edge_ids_job, graph_path, output_key, block_list, threads_per_job),
+                    mode)
+    return timer
+
+
+def _normalize(x):
+    """vu.normalize (utils/volume_utils.py:98-105): float32, min to 0, max to 1."""
+    x = np.asarray(x, dtype=np.float32).copy()
+    x -= x.min()
+    m = x.max()
+    if m > 0:
+        x /= m
+    return x
+
+
+def _accumulate_filter(input_, graph, labels, bb_local, filter_name, sigma, ignore_label, with_size, apply_in_2d):
+    """block_edge_features.py:151-168: filter response on the GPU, then one
+    accumulateInput per response channel (size column on the last one)."""
+    response = fastfilters.apply_filter(input_, filter_name, sigma, apply_in_2d=apply_in_2d)[bb_local]
+    if response.ndim == 4:
+        n_chan = response.shape[-1]
+        return np.concatenate([ndist.accumulateInput(graph, response[..., c], labels, ignore_label,
+                                                     with_size and c == n_chan - 1,
+                                                     response[..., c].min(), response[..., c].max())
+                               for c in range(n_chan)], axis=1)
+    return ndist.accumulateInput(graph, response, labels, ignore_label, with_size, response.min(), response.max())
+
+
+def _filter_block(block_id, blk, ds_in, ds_labels, ds_edges, ds_out, filters, sigmas, halo, ignore_label,
+                  apply_in_2d, channel_agglomeration):
+    """block_edge_features.py:171-238 (_accumulate_block): the block's
+    sub-graph, its labels over the inner block + 1 (positive side), the
+    normalised input with the filter halo; one row block of
+    len(filters) x len(sigmas) x 9 (+ size) columns per edge."""
+    pos = blk.blockGridPosition(block_id)
+    edges = ds_edges.read_chunk(pos)
+    if edges is None:
+        return None
+    graph = ndist.Graph(np.asarray(edges).reshape(-1, 2))
+    shape = ds_labels.shape
+    if sum(halo) > 0:
+        b = blk.getBlockWithHalo(block_id, list(halo))
+        bshape = b.outerBlock.shape
+        bb_in = tuple(slice(x, y) for x, y in zip(b.outerBlock.begin, b.outerBlock.end))
+        bb = tuple(slice(x, min(y + 1, sh)) for x, y, sh in zip(b.innerBlock.begin, b.innerBlock.end, shape))
+        bb_local = tuple(slice(x, min(y + 1, bs)) for x, y, bs in
+                         zip(b.innerBlockLocal.begin, b.innerBlockLocal.end, bshape))
+    else:
+        b = blk.getBlock(block_id)
+        bb = tuple(slice(x, min(y + 1, sh)) for x, y, sh in zip(b.begin, b.end, shape))
+        bb_in = bb
+        bb_local = slice(None)
+    if ds_in.ndim == 4:
+        bb_in = (slice(0, 3),) + bb_in
+    input_ = _normalize(ds_in[bb_in])
+    if ds_in.ndim == 4:
+        if channel_agglomeration is None:
+            raise ValueError('4-D filter input needs a channel_agglomeration')
+        input_ = getattr(np, channel_agglomeration)(input_, axis=0)
+    labels = ds_labels[bb]
+    feats = [_accumulate_filter(input_, graph, labels, bb_local, f, s, ignore_label,
+                                f == filters[-1] and s == sigmas[-1], apply_in_2d)
+             for f in filters for s in sigmas]
+    feats = np.concatenate(feats, axis=1)
+    ds_out.write_chunk(pos, feats.flatten(), True)
+    return feats.shape[1]
+
+
+def _block_features_job(input_path, input_key, labels_path, labels_key, graph_path, output_path, block_shape,
+                        ndim, is_u8, offsets, filters, sigmas, halo, apply_in_2d, channel_agglomeration, blocks):
+    """block_edge_features.py:113-148 (and :297-319 with filters)."""
+    if filters is not None:                                       # :304-319, _accumulate_with_filters
+        if offsets is not None:
+            raise ValueError('Filters and offsets are not supported')   # :310
+        if sigmas is None:
+            raise ValueError('Need sigma values')                       # :312
+        with ndist._open(input_path, 'r') as fi, ndist._open(labels_path, 'r') as fl, \
+                ndist._open(graph_path, 'r') as fg, ndist._open(output_path) as fo:
+            g = fg['s0/sub_graphs']
+            blk = blocking([0, 0, 0], list(g.attrs['shape']), list(block_shape))
+            n = None
+            for b in blocks:
+                r = _filter_block(b, blk, fi[input_key], fl[labels_key], g['edges'], fo['s0/sub_features'],
+                                  filters, sigmas, halo, bool(g.attrs['ignore_label']), apply_in_2d,
+                                  channel_agglomeration)
+                n = r if r is not None else n
+        return n
+    if ndim == 3:
+        fn = ndist.extractBlockFeaturesFromBoundaryMaps_uint8 if is_u8 else \
+            ndist.extractBlockFeaturesFromBoundaryMaps_float32
+        fn(graph_path, 's0/sub_graphs', input_path, input_key, labels_path, labels_key, blocks,
+           output_path, 's0/sub_features', increaseRoi=True)
+    else:
+        fn = ndist.extractBlockFeaturesFromAffinityMaps_uint8 if is_u8 else \
+            ndist.extractBlockFeaturesFromAffinityMaps_float32
+        fn(graph_path, 's0/sub_graphs', input_path, input_key, labels_path, labels_key, blocks,
+           output_path, 's0/sub_features', offsets)
+    return 10
+
+
+def _merge_features_job(graph_path, output_path, output_key, block_list, threads_per_job, run):
+    """merge_edge_features.py:127-147: one mergeFeatureBlocks call over the
+    job's edge range."""
+    ndist.mergeFeatureBlocks(graph_path, 's0/sub_graphs', output_path, 's0/sub_features', output_path,
+                             output_key, blockIds=block_list, edgeIdBegin=run[0], edgeIdEnd=run[1],
+                             numberOfThreads=threads_per_job)
+
+
+def edge_features_workflow(input_path, input_key, labels_path, labels_key, graph_path, graph_key, output_path,
+                           output_key, block_shape, max_jobs=1, max_jobs_merge=1, threads_per_job=16, offsets=None,
+                           timer=None, filters=None, sigmas=None, halo=(0, 0, 0), apply_in_2d=False,
+                           channel_agglomeration='mean', mode='threads'):
+    """EdgeFeaturesWorkflow: per-block features into s0/sub_features, merged
+    (E, n_features) table at ``output_key``; ``filters`` / ``sigmas`` select
+    the filter-feature branch (block_edge_features.py:297-319)."""
+    timer = timer or Timer()
+    with ndist._open(graph_path, 'r') as f:
+        shape = list(f['s0/sub_graphs'].attrs['shape'])
+        n_edges = int(f[graph_key].attrs['numberOfEdges'])
+    with ndist._open(input_path, 'r') as f:
+        ds = f[input_key]
+        dtype, ndim = ds.dtype, ds.ndim
+    block_list = blocks_in_volume(shape, block_shape)
+    with timer.stage('block_edge_features'):
+        with ndist._open(output_path) as f:                     # block_edge_features.py:61-64
+            ds = f.require_dataset('s0/sub_features', shape=shape, chunks=list(block_shape), compression='gzip',
+                                   dtype='float64')
+            ds.attrs['n_features'] = 10                           # :321-325
+        job = functools.partial(_block_features_job, input_path, input_key, labels_path, labels_key, graph_path,
+                                output_path, list(block_shape), ndim, dtype == np.uint8,
+                                None if offsets is None else [list(o) for o in offsets],
+                                None if filters is None else list(filters), None if sigmas is None else list(sigmas),
+                                tuple(halo), apply_in_2d, channel_agglomeration)
+        n_feats = [n for n in _run_jobs(job, _jobs(block_list, max_jobs), mode) if n is not None]
+        n_features = n_feats[0] if n_feats else 10
+        with ndist._open(output_path) as f:                     # job 0 writes n_features (:321-325)
+            f['s0/sub_features'].attrs['n_features'] = int(n_features)
+    with timer.stage('merge_edge_features'):
+        chunk = min(262144, n_edges)
+        with ndist._open(output_path) as f:                     # merge_edge_features.py:62-65
+            f.require_dataset(output_key, shape=(n_edges, n_features), chunks=(max(1, chunk), 1),
+                              compression='gzip', dtype='float64')
+        # edge chunks of chunk_size dealt to the merge jobs as consecutive runs
+        # (merge_edge_features.py:74-79, cluster_tasks.py:305-329); one
+        # mergeFeatureBlocks call per job over its run (:127-147)
+        n_chunks = (n_edges + chunk - 1) // max(1, chunk)
+        n_jobs = max(1, min(n_chunks, max_jobs_merge))
+        per_job = [n_chunks // n_jobs + (1 if j < n_chunks % n_jobs else 0) for j in range(n_jobs)]
+        runs, c0 = [], 0
+        for n in per_job:
+            runs.append((c0 * chunk, min(n_edges, (c0 + n) * chunk)))
+            c0 += n
+        if n_edges:
+            _run_jobs(functools.partial(_merge_features_job, graph_path, output_path, output_key, block_list,
+                                        threads_per_job), runs, mode)
+    return timer

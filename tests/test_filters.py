@@ -109,7 +109,8 @@ def test_accumulate_input(gpu, with_size, ignore):
 
 @pytest.mark.gpu
 def test_workflow_filter_branch(gpu, tmp_path):
-    from cluster_tools_amd import n5, workflow, synthetic as S
+    from cluster_tools_amd import n5, synthetic as S
+    from harness import workflow
     lab, bnd = S.generate((24, 48, 40), cell=7, seed=6)
     inp, out = str(tmp_path / 'in.n5'), str(tmp_path / 'out.n5')
     block = (12, 24, 20)

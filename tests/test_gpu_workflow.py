@@ -1,4 +1,4 @@
-"""GraphWorkflow + EdgeFeaturesWorkflow end to end (cluster_tools_amd.workflow:
+"""GraphWorkflow + EdgeFeaturesWorkflow end to end (harness/workflow.py:
 the reference's job bodies on job threads, N5 in -> N5 out), against the
 whole-volume call: BASELINE configs[0] geometry (125 x 1250 x 1250 with
 64 x 256 x 256 blocks, SURVEY 8(d)'s offline substitute) and small volumes
@@ -12,7 +12,8 @@ histograms), nodes = unique labels.
 import numpy as np
 import pytest
 
-from cluster_tools_amd import n5, rag, workflow
+from cluster_tools_amd import n5, rag
+from harness import workflow
 from cluster_tools_amd import synthetic as S
 from oracle import rag_oracle as O
 
@@ -33,13 +34,14 @@ def _write_inputs(path, lab, data, block, level=1):
         ds[:] = data
 
 
-def _run(tmp_path, lab, data, block, offsets=None, max_jobs=4, max_jobs_merge=2):
+def _run(tmp_path, lab, data, block, offsets=None, max_jobs=4, max_jobs_merge=2, mode='threads'):
     inp = str(tmp_path / 'in.n5')
     out = str(tmp_path / 'out.n5')
     _write_inputs(inp, lab, data, block)
-    t = workflow.graph_workflow(inp, 'seg', out, 'graph', block, max_jobs=max_jobs)
+    t = workflow.graph_workflow(inp, 'seg', out, 'graph', block, max_jobs=max_jobs, mode=mode)
     workflow.edge_features_workflow(inp, 'bnd', inp, 'seg', out, 'graph', out, 'features', block,
-                                    max_jobs=max_jobs, max_jobs_merge=max_jobs_merge, offsets=offsets, timer=t)
+                                    max_jobs=max_jobs, max_jobs_merge=max_jobs_merge, offsets=offsets, timer=t,
+                                    mode=mode)
     with n5.File(out, 'r') as f:
         g = f['graph']
         edges, nodes, feats = g['edges'][:], g['nodes'][:], f['features'][:]
@@ -48,11 +50,13 @@ def _run(tmp_path, lab, data, block, offsets=None, max_jobs=4, max_jobs_merge=2)
     return edges, nodes, feats, t
 
 
-@pytest.mark.parametrize('dtype', ['float32', 'uint8'])
-def test_workflow_boundary_small(gpu, tmp_path, dtype):
+@pytest.mark.parametrize('dtype,mode', [('float32', 'threads'), ('uint8', 'threads'), ('float32', 'processes')])
+def test_workflow_boundary_small(gpu, tmp_path, dtype, mode):
+    """mode 'processes': every job a spawned process, as LocalTask runs them
+    (3 job processes at a time beside the test process)."""
     lab, bnd = S.generate((40, 70, 90), cell=6, seed=51)
     data = bnd if dtype == 'float32' else np.round(bnd * 255).astype(np.uint8)
-    edges, nodes, feats, _ = _run(tmp_path, lab, data, (16, 32, 32))
+    edges, nodes, feats, _ = _run(tmp_path, lab, data, (16, 32, 32), max_jobs=3, mode=mode)
     e_ref, f_ref = O.boundary_features(lab, data)
     np.testing.assert_array_equal(edges, e_ref)
     np.testing.assert_array_equal(nodes, np.unique(lab))

@@ -496,3 +496,22 @@ def test_label_multiset_reads_as_argmax(tmp_path):
         assert ds.is_label_multiset and ds.dtype == np.uint64
         np.testing.assert_array_equal(ds[:], lab)
         np.testing.assert_array_equal(ds[3:17, 4:29, 1:25], lab[3:17, 4:29, 1:25])
+
+
+def _square_job(x):
+    if x < 0:
+        raise ValueError('negative job %d' % x)
+    return x * x
+
+
+def test_harness_job_processes_order_and_failure():
+    """harness.workflow's process mode (LocalTask's model, cluster_tasks.py:
+    528-550): one spawned process per job, results in job order, a failing
+    job fails the task with its traceback."""
+    from harness import workflow
+    assert workflow._run_jobs(_square_job, [3, 1, 2], 'processes') == [9, 1, 4]
+    assert workflow._run_jobs(_square_job, [3, 1, 2], 'threads') == [9, 1, 4]
+    with pytest.raises(RuntimeError, match='negative job -1'):
+        workflow._run_jobs(_square_job, [2, -1], 'processes')
+    with pytest.raises(ValueError):
+        workflow._run_jobs(_square_job, [1], 'fibers')
