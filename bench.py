@@ -145,7 +145,9 @@ def _config0_write_inputs(path, shape, block, cell, seed):
     as gzip N5 (level 1) -- in a child process, so the bench process itself
     has not touched the device when the process-mode jobs start (the GPU box
     allows 16 processes on the card)."""
+    import torch   # before libctg: the library then shares torch's HIP runtime (one runtime per process)
     from cluster_tools_amd import _lib, n5, rag
+    torch.cuda.set_device(0)
     _lib.init_device(0)
     lt, bt = rag.synth_volume(shape, cell=cell, seed=seed)
     lab = lt.cpu().numpy().view(np.uint64)
