@@ -178,6 +178,9 @@ def bench_config0(args):
     import shutil
     import tempfile
     from concurrent.futures import ProcessPoolExecutor
+    # torch's HIP runtime is loaded (not started) before libctg, so the thread-mode
+    # and compute-only parts below run libctg and torch on one runtime
+    import torch
     from harness import workflow
     shape, block = (125, 1250, 1250), (64, 256, 256)
     V = int(np.prod(shape))
@@ -223,9 +226,9 @@ def bench_config0(args):
         ms_p, stages_p, _, n_edges = measure('processes', CONFIG0_PROC_JOBS, 0)
         ms_t, stages_t, feat_prof, _ = measure('threads', 16, 1000)
 
-        import torch
         from cluster_tools_amd import _lib, n5, rag
         from cluster_tools_amd.blocking import blocking
+        torch.cuda.set_device(0 if args.device is None else args.device)
         _lib.init_device(0 if args.device is None else args.device)
         with n5.File(inp, 'r') as f:
             lt = torch.from_numpy(f['seg'][:].view(np.int64)).cuda()
