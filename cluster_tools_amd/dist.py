@@ -11,14 +11,18 @@ single-launch face scan over the whole slab with ``keep_stats`` so that its
 per-edge partial statistics stay mergeable.  The only exchange step of the
 path is the merge: edges are range-partitioned by their lower label ``u``
 (splitters from an all-gathered sample, so the concatenation of the rank
-shards is the globally sorted edge table), the partial rows travel in one
-``all_to_all_single`` (28 x int64 per edge: (u,v), (sum, sumsq), the 48-word
-wide record).  Only rows that leave their rank are packed and shipped, and
-only keys present on more than one rank are merged (``ctg_merge_stats``):
-every other edge is complete in its slab and keeps the features of the local
-call.  With spatially ordered labels (the reference's block-offset watershed
-ids, the synthetic volumes) that is the few edges crossing a slab boundary.
-Node lists take the same route.  Scaling is weak: per-rank slab size is fixed.
+shards is the globally sorted edge table); the rows that leave their rank
+(28 x int64 per edge: (u,v), (sum, sumsq), the 48-word wide record) and the
+node ids travel in ONE uniform-split ``all_to_all_single`` of fixed-capacity
+segments whose layout, gather indices and true counts are computed on the
+device (``ExchangePlan``: learned on the first call of a slab shape, reused
+after, regrown when a call's counts overflow it).  Each rank then merges its
+own rows with the received ones in one ``ctg_merge_stats`` call.  No count
+matrix or split list is read on the host: the first host read of a call is
+the merged result's size (with the overflow flag), then the shard offsets.
+With spatially ordered labels (the reference's block-offset watershed ids,
+the synthetic volumes) few rows leave their rank.  Scaling is weak:
+per-rank slab size is fixed.
 
 The exchange logic is backend-agnostic: ``HipBackend`` (libctg.so, the
 product path) or, in the CPU tests, an oracle-backed numpy backend with the
@@ -154,56 +158,6 @@ def _wire_device(device, group):
     return torch.device('cpu') if dist.get_backend(group) == 'gloo' else device
 
 
-def exchange(rows, send_counts, group=None, recv_counts=None):
-    """all_to_all of variable-length row blocks; returns the received rows.
-    With ``recv_counts`` (known from an earlier all_gather of the count
-    matrix) no count exchange and no host round trip happen here."""
-    world = dist.get_world_size(group)
-    dev = rows.device
-    wire = _wire_device(dev, group)
-    if recv_counts is None:
-        sc = torch.tensor(list(send_counts), dtype=torch.int64, device=wire)
-        rc = torch.empty(world, dtype=torch.int64, device=wire)
-        dist.all_to_all_single(rc, sc, group=group)
-        recv_counts = rc.cpu().tolist()
-    shape = (int(sum(recv_counts)),) + tuple(rows.shape[1:])
-    out = torch.empty(shape, dtype=rows.dtype, device=wire)
-    dist.all_to_all_single(out, rows.contiguous().to(wire), output_split_sizes=[int(c) for c in recv_counts],
-                           input_split_sizes=[int(c) for c in send_counts], group=group)
-    return out.to(dev)
-
-
-def exchange_rows_nodes(rows, e_send, e_recv, nodes, n_send, n_recv, group=None):
-    """One all_to_all for the edge rows (ROW_WORDS int64 each) and the node
-    ids: destination d gets [its rows, its node ids] as one int64 segment
-    (counts from the count matrix, known on every rank) -- one collective
-    instead of two per step."""
-    world = dist.get_world_size(group)
-    dev = rows.device
-    wire = _wire_device(dev, group)
-    rows = rows.reshape(-1, ROW_WORDS)
-    nodes = nodes.reshape(-1).to(torch.int64)
-    parts, r0, n0 = [], 0, 0
-    for d in range(world):
-        parts.append(rows[r0:r0 + int(e_send[d])].reshape(-1))
-        parts.append(nodes[n0:n0 + int(n_send[d])])
-        r0 += int(e_send[d])
-        n0 += int(n_send[d])
-    buf = torch.cat(parts).to(wire)
-    in_split = [int(e_send[d]) * ROW_WORDS + int(n_send[d]) for d in range(world)]
-    out_split = [int(e_recv[d]) * ROW_WORDS + int(n_recv[d]) for d in range(world)]
-    out = torch.empty(sum(out_split), dtype=torch.int64, device=wire)
-    dist.all_to_all_single(out, buf, output_split_sizes=out_split, input_split_sizes=in_split, group=group)
-    out = out.to(dev)
-    rr, nr, o = [], [], 0
-    for d in range(world):
-        rr.append(out[o:o + int(e_recv[d]) * ROW_WORDS])
-        o += int(e_recv[d]) * ROW_WORDS
-        nr.append(out[o:o + int(n_recv[d])])
-        o += int(n_recv[d])
-    return torch.cat(rr).reshape(-1, ROW_WORDS), torch.cat(nr)
-
-
 def all_gather_tensor(t, group=None):
     """all_gather of equal-shape tensors -> list (on t's device)."""
     wire = _wire_device(t.device, group)
@@ -213,26 +167,92 @@ def all_gather_tensor(t, group=None):
     return [x.to(t.device) for x in out]
 
 
-def _pack_uv(k):
-    """(E,2) int64 (u,v) -> one sortable int64 (labels < 2^31)."""
-    return k[:, 0] * (1 << 32) + k[:, 1]
+# Every device -> host read of the exchange goes through _host(): the count
+# of reads per call (and where they happen) is what the tests check -- a call
+# that reuses its ExchangePlan reads nothing before the result-size read.
+host_reads = []
 
 
-def _merge_sorted(ka, fa, kb, fb):
-    """Merge two (u,v)-sorted row sets with disjoint keys (the local-only rows
-    and the merged shared rows) by scatter, not a sort of the whole shard."""
-    pa, pb = _pack_uv(ka), _pack_uv(kb)
-    na, nb = pa.shape[0], pb.shape[0]
-    dev = ka.device
-    pos_a = torch.arange(na, device=dev) + torch.searchsorted(pb, pa)
-    pos_b = torch.arange(nb, device=dev) + torch.searchsorted(pa, pb)
-    k = torch.empty((na + nb,) + tuple(ka.shape[1:]), dtype=ka.dtype, device=dev)
-    f = torch.empty((na + nb,) + tuple(fa.shape[1:]), dtype=fa.dtype, device=dev)
-    k[pos_a] = ka
-    k[pos_b] = kb
-    f[pos_a] = fa
-    f[pos_b] = fb
-    return {'edges': k, 'features': f}
+def _host(t, where):
+    host_reads.append(where)
+    return t.cpu()
+
+
+class ExchangePlan:
+    """Per-destination capacities of the uniform all_to_all (rows and node
+    ids).  The first call of a (group, slab shape) learns them from the exact
+    count matrix (one host read) with 50 % headroom; later calls reuse them
+    and never read counts on the host: a call whose counts exceed a capacity
+    notices it at the result-size read (the overflow flag rides along) and
+    redoes the exchange with capacities learned from that call."""
+
+    def __init__(self, cap_rows=0, cap_nodes=0):
+        self.cap_rows = int(cap_rows)
+        self.cap_nodes = int(cap_nodes)
+
+    @staticmethod
+    def from_counts(max_rows, max_nodes):
+        return ExchangePlan(max_rows + max_rows // 2 + 64, max_nodes + max_nodes // 2 + 64)
+
+
+_plans = {}
+
+
+def _plan_key(group, shape, offsets):
+    return (id(group), dist.get_world_size(group), tuple(shape), None if offsets is None else
+            tuple(map(tuple, np.asarray(offsets).reshape(-1, 3).tolist())))
+
+
+NODE_EMPTY = -1           # node id of an empty slot: 2^64 - 1, last in unsigned order (never a real node id
+                          # here: the volume's labels would need the full uint64 range)
+
+
+def _uniform_exchange(keys, sums, recs, nodes, e_start, e_counts, n_start, n_counts, plan,
+                      rank, group):
+    """Rows and node ids to their owners in ONE uniform-split all_to_all_single.
+
+    Destination d gets a fixed-size segment: [true row count, true node
+    count, cap_rows rows of ROW_WORDS int64, cap_nodes node ids].  Empty
+    slots hold key (0, 0) with a zero record (no ADJ bit: the merge drops
+    them) and node id NODE_EMPTY.  Segment layout, gather indices and the overflow flag are
+    computed on the device; nothing is read on the host here.
+    Returns (received rows, received node ids, overflow flag (device))."""
+    world = dist.get_world_size(group)
+    dev = keys.device
+    wire = _wire_device(dev, group)
+    cr, cn = plan.cap_rows, plan.cap_nodes
+    n, nn = keys.shape[0], nodes.shape[0]
+    j = torch.arange(cr, device=dev)
+    src = e_start.reshape(-1, 1) + j.reshape(1, -1)                   # (world, cr)
+    ok = j.reshape(1, -1) < e_counts.reshape(-1, 1)
+    ok[rank] = False                                                  # this rank's own rows stay
+    src = torch.clamp(src, max=max(n - 1, 0)).reshape(-1)
+    if n:
+        rows = pack_rows(keys.index_select(0, src), sums.index_select(0, src), recs.index_select(0, src))
+    else:
+        rows = torch.zeros((world * cr, ROW_WORDS), dtype=torch.int64, device=dev)
+    ok = ok.reshape(-1, 1)
+    rows = torch.where(ok, rows, torch.zeros_like(rows)).reshape(world, cr * ROW_WORDS)   # empty slot: key (0, 0)
+    jn = torch.arange(cn, device=dev)
+    nsrc = torch.clamp(n_start.reshape(-1, 1) + jn.reshape(1, -1), max=max(nn - 1, 0)).reshape(-1)
+    nok = jn.reshape(1, -1) < n_counts.reshape(-1, 1)
+    nok[rank] = False
+    nv = nodes.index_select(0, nsrc) if nn else torch.zeros(world * cn, dtype=torch.int64, device=dev)
+    nv = torch.where(nok.reshape(-1), nv, torch.full_like(nv, NODE_EMPTY)).reshape(world, cn)
+    hdr = torch.stack([e_counts, n_counts], dim=1).to(torch.int64)     # true counts: the receiver's check
+    buf = torch.cat([hdr, rows, nv], dim=1).contiguous()
+    out = torch.empty_like(buf, device=wire)
+    dist.all_to_all_single(out, buf.to(wire), group=group)
+    out = out.to(dev)
+    got_e, got_n = out[:, 0].clone(), out[:, 1].clone()
+    got_e[rank] = 0
+    got_n[rank] = 0
+    over = torch.logical_or((got_e > cr).any(), (got_n > cn).any()).to(torch.int64).reshape(1)
+    # the row counts also size the next plan (max over this rank's senders)
+    over = torch.cat([over, got_e.max().reshape(1), got_n.max().reshape(1)])
+    rk = out[:, 2:2 + cr * ROW_WORDS].reshape(-1, ROW_WORDS)
+    rn = out[:, 2 + cr * ROW_WORDS:].reshape(-1)
+    return rk, rn, over
 
 
 def _tensor(x, like):
@@ -282,7 +302,7 @@ class DistResult:
 def _exclusive_offsets(n_locals, group, device):
     """[(offset of this rank, total)] for each local count, one all_gather."""
     t = torch.tensor(list(n_locals), dtype=torch.int64, device=device)
-    allc = torch.stack(all_gather_tensor(t, group)).cpu().tolist()
+    allc = _host(torch.stack(all_gather_tensor(t, group)), 'offsets').tolist()
     r = dist.get_rank(group)
     return [(sum(row[k] for row in allc[:r]), sum(row[k] for row in allc)) for k in range(len(n_locals))]
 
@@ -307,7 +327,7 @@ def check_slab_halo(shape, offsets, own_begin, own_end):
 
 
 def rag_features_distributed(labels, data=None, offsets=None, own_begin=None, own_end=None,
-                             ignore_label=False, hist_range=(0.0, 1.0), group=None, backend=None):
+                             ignore_label=False, hist_range=(0.0, 1.0), group=None, backend=None, plan=None):
     """Global RAG + edge features of a z-slab-partitioned volume.
 
     Every rank passes its slab (plus the halo planes below it, excluded via
@@ -315,11 +335,20 @@ def rag_features_distributed(labels, data=None, offsets=None, own_begin=None, ow
     edge rows are rows [edge_offset, edge_offset + n_edges) of the global
     sorted edge table (same for nodes).
 
-    Collectives: one all_gather of the splitter samples, one all_gather of
-    the (edge, node) send-count matrix -- the only host round trip before the
-    data moves --, one all_to_all of the edge rows and node ids together, and
-    the all_gather of the shard sizes.  Splitters and counts are computed on the
-    wire device, so with RCCL nothing but the count matrix leaves HBM.
+    Device-resident exchange (RCCL moves HBM tensors; nothing is read on the
+    host before the merged result's size):
+      1. local partial table with mergeable statistics (one library call);
+      2. one all_gather of splitter samples -> range splitters on u (device);
+      3. per-destination row / node counts and gather indices (device);
+      4. ONE uniform-split all_to_all_single of fixed-capacity segments
+         (``ExchangePlan``) carrying rows, node ids and the true counts;
+      5. one merge of this rank's own rows with the received ones
+         (``ctg_merge_stats``: Chan's rule on the shifted sums, histograms add);
+      6. one all_reduce of the overflow flag, read with the result size, and
+         the all_gather of the shard sizes.
+    A plan that proves too small (flag set on any rank) is regrown from the
+    true counts and the exchange redone; the first call of a slab shape
+    learns its plan that way.
     """
     shape = tuple(labels.shape)
     if world_size_of(group) > 1:
@@ -327,84 +356,77 @@ def rag_features_distributed(labels, data=None, offsets=None, own_begin=None, ow
     backend = backend or HipBackend()
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
-    keys, sums, recs, nodes, info, feats = backend.local(labels, data, offsets, own_begin, own_end,
-                                                         ignore_label, hist_range)
+    keys, sums, recs, nodes, info, _feats = backend.local(labels, data, offsets, own_begin, own_end,
+                                                          ignore_label, hist_range)
     dev = keys.device
     wire = _wire_device(dev, group)
     n = keys.shape[0]
-    nodes = nodes.reshape(-1)
+    nodes = nodes.reshape(-1).to(torch.int64)
     # splitters on u (unsigned order) from an evenly spaced sample of the
-    # sorted local keys; the signed min / max of every label ride along
-    # (the packed (u,v) fast path needs 0 <= label < 2^31)
+    # sorted local keys
     ou = _ordered(keys[:, 0]) if n else keys[:, 0]
     if n > 0:
         idx = torch.div(torch.arange(N_SAMPLES, device=dev, dtype=torch.int64) * n, N_SAMPLES,
                         rounding_mode='floor')
         samp = ou.index_select(0, idx)
-        lo = torch.minimum(keys.min(), nodes.min() if nodes.numel() else keys.min()).reshape(1)
-        hi = torch.maximum(keys.max(), nodes.max() if nodes.numel() else keys.max()).reshape(1)
     else:
         samp = torch.zeros(N_SAMPLES, dtype=torch.int64, device=dev)
-        z = nodes.min().reshape(1) if nodes.numel() else torch.zeros(1, dtype=torch.int64, device=dev)
-        lo = z
-        hi = nodes.max().reshape(1) if nodes.numel() else z
-    meta = torch.cat([samp, torch.tensor([n], dtype=torch.int64, device=dev), lo, hi]).to(wire)
-    g = torch.stack(all_gather_tensor(meta, group))
+    meta = torch.cat([samp, torch.full((1,), n, dtype=torch.int64, device=dev)]).to(wire)
+    g = torch.stack(all_gather_tensor(meta, group)).to(dev)
     splitters = weighted_splitters_t(g[:, :N_SAMPLES], g[:, N_SAMPLES], world)
-    packable = torch.logical_and(g[:, N_SAMPLES + 1].min() >= 0, g[:, N_SAMPLES + 2].max() < (1 << 31))
-    onodes = _ordered(nodes)
-    e_counts = split_counts_t(ou.to(wire), splitters)
-    n_counts = split_counts_t(onodes.to(wire), splitters)
-    mine = torch.cat([e_counts, n_counts, packable.reshape(1).to(torch.int64)])
-    cm = torch.stack(all_gather_tensor(mine, group)).cpu()         # (world, 2*world + 1): the host round trip
-    packable = bool(cm[:, 2 * world].min().item())
-    e_send = cm[rank, :world].tolist()
-    n_send = cm[rank, world:2 * world].tolist()
-    e_recv_all = cm[:, rank].tolist()
-    n_recv = cm[:, world + rank].tolist()
+    e_counts = split_counts_t(ou, splitters)
+    n_counts = split_counts_t(_ordered(nodes), splitters)
+    zero = torch.zeros(1, dtype=torch.int64, device=dev)
+    e_start = torch.cat([zero, torch.cumsum(e_counts, 0)[:-1]])
+    n_start = torch.cat([zero, torch.cumsum(n_counts, 0)[:-1]])
+    # this rank's own rows / node ids stay in place; every other one is masked
+    # to an empty slot (SENTINEL-free: key (0, 0) with a zero record is never
+    # an edge, and the merge drops rows without the ADJ bit)
+    ar = torch.arange(n, device=dev)
+    own = (ar >= e_start[rank]) & (ar < e_start[rank] + e_counts[rank])
+    own_keys = torch.where(own.reshape(-1, 1), keys, torch.zeros_like(keys))
+    own_sums = torch.where(own.reshape(-1, 1), sums.reshape(n, 2), torch.zeros_like(sums.reshape(n, 2)))
+    own_recs = torch.where(own.reshape(-1, 1), recs.reshape(n, WIDE_WORDS), torch.zeros_like(recs.reshape(n, WIDE_WORDS)))
+    arn = torch.arange(nodes.shape[0], device=dev)
+    own_n = (arn >= n_start[rank]) & (arn < n_start[rank] + n_counts[rank])
+    own_nodes = torch.where(own_n, nodes, torch.full_like(nodes, NODE_EMPTY))
 
-    if not packable:
-        # general labels: every row goes to the owner of its u and is merged there
-        rows = pack_rows(keys, sums, recs)
-        recv, nrecv = exchange_rows_nodes(rows, e_send, e_recv_all, nodes, n_send, n_recv, group)
-        rk, rs, rr = unpack_rows(recv)
-        me, mf = backend.merge(rk, rs, rr, hist_range)
-        merged = {'edges': me, 'features': mf}
-    else:
-        # rows of other owners leave; this rank's own block stays in place
-        lo_i = sum(e_send[:rank])
-        hi_i = lo_i + e_send[rank]
-        send = list(e_send)
-        send[rank] = 0
-        recv_counts = list(e_recv_all)
-        recv_counts[rank] = 0
-        out_k = torch.cat([keys[:lo_i], keys[hi_i:]])
-        out_rows = pack_rows(out_k, torch.cat([sums[:lo_i], sums[hi_i:]]), torch.cat([recs[:lo_i], recs[hi_i:]]))
-        recv, nrecv = exchange_rows_nodes(out_rows, send, recv_counts, nodes, n_send, n_recv, group)
-        lk, ls, lr, lf = keys[lo_i:hi_i], sums[lo_i:hi_i], recs[lo_i:hi_i], feats[lo_i:hi_i]
-        if recv.shape[0] == 0:
-            shared = torch.zeros(lk.shape[0], dtype=torch.bool, device=dev)
-        else:
-            rk, rs, rr = unpack_rows(recv)
-            shared = torch.isin(_pack_uv(lk), _pack_uv(rk))
-        # local-only keys are final; with affinities a key must have been seen
-        # on a nearest-neighbour face (ADJ bit of its wide record)
-        keep = ~shared
-        if offsets is not None:
-            keep &= lr[:, 42] < 0
-        if recv.shape[0] == 0:
-            merged = {'edges': lk[keep], 'features': lf[keep]}
-        else:
-            me, mf = backend.merge(torch.cat([rk, lk[shared]]), torch.cat([rs, ls[shared]]),
-                                   torch.cat([rr, lr[shared]]), hist_range)
-            me = _tensor(me, lk)
-            mf = _tensor(mf, lf)
-            merged = _merge_sorted(lk[keep], lf[keep], me, mf)
+    key = _plan_key(group, shape, offsets)
+    if plan is None:
+        plan = _plans.get(key)
+    learn = plan is None
+    if learn:
+        plan = ExchangePlan(0, 0)
+    while True:
+        rk, rn, over = _uniform_exchange(keys, sums, recs, nodes, e_start, e_counts, n_start, n_counts,
+                                         plan, rank, group)
+        over = over.to(wire)
+        dist.all_reduce(over, op=dist.ReduceOp.MAX, group=group)
+        if learn:
+            # no plan yet: learn the capacities from the true counts now (the
+            # only host read before the merge, first call of a shape only)
+            ov = _host(over, 'plan')
+            plan = ExchangePlan.from_counts(int(ov[1]), int(ov[2]))
+            learn = False
+            if int(ov[0]):
+                continue
+        rks, rss, rrs = unpack_rows(rk)
+        me, mf = backend.merge(torch.cat([own_keys, rks]), torch.cat([own_sums, rss]),
+                               torch.cat([own_recs, rrs]), hist_range)
+        # the result-size read: the merge has returned its size; the overflow
+        # flag (all ranks agree on it) comes to the host with it
+        ov = _host(over, 'result')
+        if int(ov[0]):
+            plan = ExchangePlan.from_counts(int(ov[1]), int(ov[2]))
+            continue
+        break
+    _plans[key] = plan
+    merged = {'edges': _tensor(me, keys), 'features': _tensor(mf, keys)}
     n_loc = int(merged['edges'].shape[0])
-
-    # nodes went to the same ranges in the rows' all_to_all
-    node_shard = backend.unique(nrecv)
-
+    # nodes went to the same ranges in the all_to_all; one NODE_EMPTY is
+    # appended so the sorted unique ids always end with exactly one of it
+    node_shard = backend.unique(torch.cat([own_nodes, rn, torch.full((1,), NODE_EMPTY, dtype=torch.int64,
+                                                                       device=dev)]))[:-1]
     (e_off, e_tot), (n_off, n_tot) = _exclusive_offsets([n_loc, int(node_shard.shape[0])], group, dev)
     return DistResult(merged, node_shard, e_off, e_tot, n_off, n_tot, info)
 

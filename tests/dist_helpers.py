@@ -78,10 +78,18 @@ class OracleBackend:
         if k.shape[0] == 0:
             return torch.zeros((0, 2), dtype=torch.int64), torch.zeros((0, O.N_FEATURES), dtype=torch.float64)
         edges, inv = O._unique_pairs(k, return_inverse=True)
-        st = decode_stats(sums.numpy(), recs.numpy().view(np.uint32))
+        rec = recs.numpy().view(np.uint32)
+        st = decode_stats(sums.numpy(), rec)
         merged = O.merge_feature_stats([(inv, st)], edges.shape[0], hist_range[0], hist_range[1])
         feats = O.finalize_features(merged, hist_range[0], hist_range[1])
-        return torch.from_numpy(edges.astype(np.int64)), torch.from_numpy(np.ascontiguousarray(feats))
+        # ctg_merge_stats keeps only keys with the ADJ bit on some row (need_adj):
+        # the exchange's empty slots (key (0, 0), zero record) disappear here
+        adj = np.zeros(edges.shape[0], bool)
+        np.logical_or.at(adj, inv, (rec[:, 42] & ADJ) != 0)
+        return (torch.from_numpy(edges[adj].astype(np.int64)),
+                torch.from_numpy(np.ascontiguousarray(feats[adj])))
 
     def unique(self, values):
-        return torch.from_numpy(np.unique(values.numpy()))
+        """sorted unique ids in unsigned order (as ctg_unique_labels)"""
+        u = np.unique(values.numpy().view(np.uint64))
+        return torch.from_numpy(u.view(np.int64))

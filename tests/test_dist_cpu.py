@@ -168,3 +168,42 @@ def test_device_splitters_match_numpy_restatement():
         cw = np.cumsum(w)
         idx = np.minimum(np.searchsorted(cw, cw[-1] * np.arange(1, world) / world, side='left'), v.size - 1)
         np.testing.assert_array_equal(sp, v[idx])
+
+
+def _plan_worker(rank, world, port, outdir):
+    """Three calls on the same slab: the first learns the ExchangePlan, the
+    second reuses it (no host read before the result-size read), the third
+    starts from a plan too small for its counts (overflow -> regrow -> redo)."""
+    import torch.distributed as dist
+    from tests.dist_helpers import OracleBackend
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    shape = (8 * world, 30, 28)
+    lab, bnd = _volume(shape, 5, False)
+    z0 = [shape[0] * r // world for r in range(world + 1)]
+    halo = 1 if rank > 0 else 0
+    sl = slice(z0[rank] - halo, z0[rank + 1])
+    args = (np.ascontiguousarray(lab[sl]), np.ascontiguousarray(bnd[sl]))
+    outs, reads = [], []
+    for call, plan in enumerate([None, None, cdist.ExchangePlan(1, 1)]):
+        del cdist.host_reads[:]
+        res = cdist.rag_features_distributed(*args, own_begin=(halo, 0, 0), backend=OracleBackend(), plan=plan)
+        reads.append(list(cdist.host_reads))
+        outs.append((np.asarray(res.edges()), np.asarray(res.features()), res.node_shard.numpy()))
+    for a in outs[1:]:
+        for x, y in zip(a, outs[0]):
+            np.testing.assert_array_equal(x, y)
+    np.save(os.path.join(outdir, 'reads%d.npy' % rank), np.array(['|'.join(r) for r in reads]))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize('world', [2, 4])
+def test_exchange_plan_reuse_and_overflow(tmp_path, world):
+    mp.spawn(_plan_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    for r in range(world):
+        reads = list(np.load(tmp_path / ('reads%d.npy' % r)))
+        # (the shard offsets are read after the result size)
+        assert reads[0] == 'plan|result|offsets'           # first call of the shape: learns its plan
+        assert reads[1] == 'result|offsets'                # plan reused: nothing read before the result size
+        assert reads[2] == 'result|result|offsets'         # too small: overflow seen with the result, redone
