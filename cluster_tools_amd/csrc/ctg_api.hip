@@ -18,6 +18,7 @@
 namespace ctg {
 hipError_t launch_face_scan(const ScanParams& P, const RecordBuf& R, Counters* C, hipStream_t s);
 int scan_tile_rows();
+hipError_t launch_narrow_labels(const uint64_t* L, uint32_t* out, int64_t n, uint32_t* ovf, hipStream_t s);
 hipError_t launch_density(const void* L, int label_bits, const int64_t* shape, int n_rows, uint32_t* out,
                           hipStream_t s);
 hipError_t launch_unique_tiles(const uint64_t* L, const int64_t* shape, const int64_t* b, const int64_t* e,
@@ -172,7 +173,7 @@ static hipError_t ws_init(Workspace& w) {
     if (e != hipSuccess) return e;
     e = hipHostMalloc(&w.small_host, 64 * sizeof(unsigned int), hipHostMallocDefault);
     if (e != hipSuccess) return e;
-    for (int i = 0; i < 8; ++i) hipEventCreate(&w.ev[i]);
+    for (int i = 0; i < 10; ++i) hipEventCreate(&w.ev[i]);
     w.events = true;
     return hipSuccess;
 }
@@ -872,6 +873,47 @@ int ctg_rag_features(const void* labels, int label_bits, const void* data, int d
     bool long_range = false;
     for (int c = 0; c < P.n_channels; ++c)
         long_range |= std::abs(P.offsets[c][0]) + std::abs(P.offsets[c][1]) + std::abs(P.offsets[c][2]) > 1;
+
+    // Long-range affinity scans gather the partner label of every channel at
+    // p + o_c: 4-B gathers on the 8-B-strided uint64 array use half of every
+    // line they pull.  One narrowing pass (12 B / voxel) gives them -- and the
+    // graph pass and the scan's own plane loads -- a u32 copy when every label
+    // is < 2^32 (checked by the same pass; otherwise the 64-bit path and its
+    // dense relabelling run as before).  CTG_NARROW_LABELS: 0 never, 2 for
+    // every affinity call (A/B), default long-range calls.
+    struct DevBuf {
+        void* p = nullptr;
+        ~DevBuf() { dfree(p); }
+    } l32;
+    {
+        const char* nl = getenv("CTG_NARROW_LABELS");
+        const int mode = nl ? atoi(nl) : 1;
+        const bool want = label_bits == 64 && V > 0 && P.n_channels > 0 &&
+                          (mode == 2 || (mode == 1 && long_range)) && ((uintptr_t)dl % 16) == 0;
+        if (data) w.last_ms[7] = 0.0;   // graph-only calls (the adjacency pass) keep the caller's value
+        if (want) {
+            l32.p = dalloc((size_t)V * 4);
+            if (l32.p) {
+                CTG_CHECK(hipMemsetAsync(w.small + 16, 0, 4, s));
+                if (w.profiling) hipEventRecord(w.ev[8], s);
+                CTG_CHECK(launch_narrow_labels((const uint64_t*)dl, (uint32_t*)l32.p, V, w.small + 16, s));
+                if (w.profiling) hipEventRecord(w.ev[9], s);
+                CTG_CHECK(hipMemcpyAsync(w.small_host + 16, w.small + 16, 4, hipMemcpyDeviceToHost, s));
+                CTG_CHECK(hipStreamSynchronize(s));
+                if (w.profiling) {
+                    float nms = 0.f;
+                    hipEventElapsedTime(&nms, w.ev[8], w.ev[9]);
+                    w.last_ms[7] = nms;
+                }
+                if (w.small_host[16] == 0) {
+                    dl = l32.p;
+                    label_bits = 32;
+                    P.labels = dl;
+                    P.label_bits = 32;
+                }
+            }
+        }
+    }
     if (long_range && !(flags & CTG_NO_ADJ_FILTER) && V > 0) {
         rc = ctg_rag_features(dl, label_bits, nullptr, CTG_DATA_NONE, 0, nullptr, shape, own_begin, own_end, 0,
                               hist_lo, hist_hi, 0, CTG_MEM_DEVICE, stream, &adj_graph);

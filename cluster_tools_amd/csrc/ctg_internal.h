@@ -206,9 +206,9 @@ struct Workspace {
     void* stage[2] = {nullptr, nullptr};
     size_t stage_bytes[2] = {0, 0};
     // timing
-    hipEvent_t ev[8];
+    hipEvent_t ev[10];   // 0..6 phases of a call; 8, 9 bracket the label narrowing (prep)
     bool events = false;
-    double last_ms[8] = {0};
+    double last_ms[8] = {0};   // scan, pack, sort, segment, reduce, nodes, total, narrow
     int64_t last_records = 0, last_direct = 0;
     int profiling = 0;
 };

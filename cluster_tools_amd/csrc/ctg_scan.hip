@@ -1080,6 +1080,42 @@ hipError_t launch_density(const void* L, int label_bits, const int64_t* shape, i
     return hipGetLastError();
 }
 
+// uint64 labels -> their low halves (long-range affinity scans gather the
+// partner label at p + o_c for every channel: from a u32 array each 64-B line
+// serves 16 labels instead of 8).  Four labels per thread (two 16-B loads,
+// one 16-B store); the OR of every high half lands in *ovf (labels >= 2^32:
+// the caller keeps the 64-bit path and its dense relabelling).
+__global__ __launch_bounds__(256) void k_narrow_labels(const uint4* __restrict__ L, uint4* __restrict__ out,
+                                                        int64_t n4, const uint64_t* __restrict__ tail_in,
+                                                        uint32_t* __restrict__ tail_out, int tail,
+                                                        uint32_t* __restrict__ ovf) {
+    uint32_t hi = 0;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+        const uint4 a = L[2 * i];
+        const uint4 b = L[2 * i + 1];
+        hi |= a.y | a.w | b.y | b.w;
+        out[i] = make_uint4(a.x, a.z, b.x, b.z);
+    }
+    if (blockIdx.x == 0 && (int)threadIdx.x < tail) {
+        const uint64_t l = tail_in[threadIdx.x];
+        hi |= (uint32_t)(l >> 32);
+        tail_out[threadIdx.x] = (uint32_t)l;
+    }
+    if (__ballot(hi != 0) && (threadIdx.x & (WAVE - 1)) == 0) atomicOr(ovf, 1u);
+}
+
+hipError_t launch_narrow_labels(const uint64_t* L, uint32_t* out, int64_t n, uint32_t* ovf, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    const int64_t n4 = n / 4;
+    const int tail = (int)(n - n4 * 4);
+    int64_t grid = std::min<int64_t>((n4 + 255) / 256, 256 * 16);
+    grid = std::max<int64_t>(grid, 1);
+    hipLaunchKernelGGL(k_narrow_labels, dim3((unsigned)grid), dim3(256), 0, s, (const uint4*)L, (uint4*)out, n4,
+                       L + n4 * 4, out + n4 * 4, tail, ovf);
+    return hipGetLastError();
+}
+
 int scan_tile_rows() { return WG_ROWS; }
 
 // ---------------------------------------------------------------------------

@@ -546,7 +546,8 @@ def set_profiling(on=True):
 
 
 def last_timings():
-    """Device ms of the last rag call: scan, pack, sort, segment, reduce, nodes, total."""
-    buf = (ctypes.c_double * 7)()
-    L.check(L.load().ctg_last_timings(buf, 7), 'ctg_last_timings')
-    return dict(zip(['scan', 'pack', 'sort', 'segment', 'reduce', 'nodes', 'total'], list(buf)))
+    """Device ms of the last rag call: scan, pack, sort, segment, reduce, nodes, total, and narrow (the
+    uint64 -> u32 label pass of long-range affinity calls, before the scan; 0 when it did not run)."""
+    buf = (ctypes.c_double * 8)()
+    L.check(L.load().ctg_last_timings(buf, 8), 'ctg_last_timings')
+    return dict(zip(['scan', 'pack', 'sort', 'segment', 'reduce', 'nodes', 'total', 'narrow'], list(buf)))
