@@ -879,15 +879,18 @@ int ctg_rag_features(const void* labels, int label_bits, const void* data, int d
     // line they pull.  One narrowing pass (12 B / voxel) gives them -- and the
     // graph pass and the scan's own plane loads -- a u32 copy when every label
     // is < 2^32 (checked by the same pass; otherwise the 64-bit path and its
-    // dense relabelling run as before).  CTG_NARROW_LABELS: 0 never, 2 for
-    // every affinity call (A/B), default long-range calls.
+    // dense relabelling run as before).  CTG_NARROW_LABELS: 1 long-range
+    // calls, 2 every affinity call; default 0 (off): measured on configs[3]
+    // 1024^3, the 12-channel scan went 45.39 -> 45.03 ms for a 2.70 ms pass,
+    // the 3-channel scan 8.91 -> 9.06 ms -- the channel loop is bound by its
+    // folds (4.2e9 samples), not by the lines the gathers pull.
     struct DevBuf {
         void* p = nullptr;
         ~DevBuf() { dfree(p); }
     } l32;
     {
         const char* nl = getenv("CTG_NARROW_LABELS");
-        const int mode = nl ? atoi(nl) : 1;
+        const int mode = nl ? atoi(nl) : 0;
         const bool want = label_bits == 64 && V > 0 && P.n_channels > 0 &&
                           (mode == 2 || (mode == 1 && long_range)) && ((uintptr_t)dl % 16) == 0;
         if (data) w.last_ms[7] = 0.0;   // graph-only calls (the adjacency pass) keep the caller's value

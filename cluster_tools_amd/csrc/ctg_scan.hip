@@ -442,6 +442,93 @@ __device__ __forceinline__ void fold_stats(Table& T, const StageT& e, int s, uin
     }
 }
 
+// lane pairs (2i, 2i+1) / (i, i^2) exchange a value (DPP quad_perm [1,0,3,2] / [2,3,0,1])
+__device__ __forceinline__ uint32_t dpp_x1(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0xB1, 0xf, 0xf, false);
+}
+__device__ __forceinline__ uint32_t dpp_x2(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x4E, 0xf, 0xf, false);
+}
+template <int X>
+__device__ __forceinline__ double dpp_f64(double v) {
+    const uint64_t b = (uint64_t)__double_as_longlong(v);
+    const uint32_t lo = X == 1 ? dpp_x1((uint32_t)b) : dpp_x2((uint32_t)b);
+    const uint32_t hi = X == 1 ? dpp_x1((uint32_t)(b >> 32)) : dpp_x2((uint32_t)(b >> 32));
+    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+
+// Boundary-map fold with same-key lanes combined first.  Faces of one site
+// arrive in x order, so runs of lanes hold the same key (a cell pair's y / z
+// boundary spans several voxels along x); their LDS atomics to one entry
+// serialise in the LDS banks.  Within each aligned lane pair, then quad, lanes
+// that resolved to the same table slot add their shifted sums and fold their
+// min / max with two DPP exchanges, and only the group's first lane issues
+// the sum / sum-of-squares / min / max atomics (the histogram adds stay per
+// lane: two samples rarely share a slot word with their neighbours').
+#ifndef CTG_PAIR_FOLD
+#define CTG_PAIR_FOLD 1
+#endif
+template <bool FAST40, typename StageT, int NPER>
+__device__ __forceinline__ void fold_boundary_grouped(Table& T, const StageT (&e)[NPER], const int (&slot)[NPER],
+                                                      const uint32_t (&pv)[NPER], int lane, RecordBuf R, Counters* C,
+                                                      double scale, double offset) {
+#pragma unroll
+    for (int i = 0; i < NPER; ++i) {
+        const int sl = slot[i];
+        if (sl == -1) {   // table full: a direct record, no grouping (rare)
+            bool dummy = false;
+            fold_stats<MODE_BOUNDARY, FAST40, false, StageT>(T, e[i], -1, PIV_EMPTY, R, C, scale, offset, dummy, 0);
+        }
+        const bool v = sl >= 0;
+        const float a = __uint_as_float(e[i].z), b = __uint_as_float(e[i].w);
+        const double da = (double)a, db = (double)b;
+        if (v) hist_add2(T, sl, sample_slot<FAST40>(da, scale, offset), sample_slot<FAST40>(db, scale, offset));
+        // the entry's pivot: the first sample that claims the empty word (CAS)
+        uint32_t p = pv[i];
+        if (v && p == PIV_EMPTY) {
+            const uint32_t mine = pivot_bits(a);
+            const uint32_t old = atomicCAS(&T.w[sl][24], PIV_EMPTY, mine);
+            p = old == PIV_EMPTY ? mine : old;
+        }
+        const double dp = (double)__uint_as_float(p);
+        const double ea = da - dp, eb = db - dp;
+        double sm = ea + eb, sq = ea * ea + eb * eb;
+        uint32_t mn = f2ord(fminf(a, b)), mx = f2ord(fmaxf(a, b));
+        // groups: every lane active here (no divergent branch encloses this);
+        // a lane without a slot gets a key no other lane has
+        const uint32_t key = v ? (uint32_t)sl : 0x80000000u | (uint32_t)lane;
+        const bool g1 = dpp_x1(key) == key;
+        {
+            const double s1 = dpp_f64<1>(sm), q1 = dpp_f64<1>(sq);
+            const uint32_t mn1 = dpp_x1(mn), mx1 = dpp_x1(mx);
+            sm = g1 ? sm + s1 : sm;
+            sq = g1 ? sq + q1 : sq;
+            mn = g1 ? min(mn, mn1) : mn;
+            mx = g1 ? max(mx, mx1) : mx;
+        }
+        // both exchanges unconditional: under a short-circuit && the compiler
+        // runs a DPP with part of the wave masked off, and a masked source
+        // lane reads as the destination's own value
+        const uint32_t g1_x2 = dpp_x2(g1 ? 1u : 0u), key_x2 = dpp_x2(key);
+        const bool g2 = g1 & (g1_x2 != 0u) & (key_x2 == key);
+        {
+            const double s2 = dpp_f64<2>(sm), q2 = dpp_f64<2>(sq);
+            const uint32_t mn2 = dpp_x2(mn), mx2 = dpp_x2(mx);
+            sm = g2 ? sm + s2 : sm;
+            sq = g2 ? sq + q2 : sq;
+            mn = g2 ? min(mn, mn2) : mn;
+            mx = g2 ? max(mx, mx2) : mx;
+        }
+        const bool lead = !(g1 && (lane & 1)) && !(g2 && (lane & 2));
+        if (v && lead) {
+            atomicMin(&T.w[sl][22], mn);
+            atomicMax(&T.w[sl][23], mx);
+            atomicAdd(&T.sum[sl], sm);
+            atomicAdd(&T.sq[sl], sq);
+        }
+    }
+}
+
 // Fold the wave's nb staged entries into the LDS edge table: NPER entries per
 // lane (lane, lane+64, ...), their stage reads and home-bucket reads issued
 // together so the LDS round trips of the entries overlap.
@@ -503,6 +590,12 @@ __device__ __forceinline__ void fold_batch(Table& T, const StageT* __restrict__ 
         if (MODE != MODE_GRAPH && slot[i] >= 0)
             pv[i] = __hip_atomic_load(&T.w[slot[i]][24], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
+#if CTG_PAIR_FOLD
+    if constexpr (MODE == MODE_BOUNDARY && !BATCH) {
+        fold_boundary_grouped<FAST40, StageT, NPER>(T, e, slot, pv, lane, R, C, scale, offset);
+        return;
+    }
+#endif
 #pragma unroll
     for (int i = 0; i < NPER; ++i)
         if (slot[i] != -2)
