@@ -161,9 +161,14 @@ def _config0_write_inputs(path, shape, block, cell, seed):
     return sum(os.path.getsize(os.path.join(r, fn)) for r, _, fs in os.walk(path) for fn in fs)
 
 
-# job processes of the process-mode graph task: the GPU box allows 16
-# processes on the card, and the bench process joins them in thread mode
-CONFIG0_PROC_JOBS = 15
+# Job processes per task in process mode.  'gpu': one job per task -- each job
+# is a GPU process, and creating / tearing down a device context costs ~60 ms
+# that the driver serialises across processes (15 graph jobs exit in ~0.9 s),
+# while one job runs all 50 blocks in ~0.1 s of device time; 'cpu_layout': the
+# job counts of the CPU reference's layout (one job per core: 15 graph jobs,
+# the GPU box allows 16 processes on the card), reported beside it.
+CONFIG0_PROC_LAYOUTS = {'gpu': dict(graph=1, features=1, merge=1),
+                        'cpu_layout': dict(graph=15, features=1, merge=4)}
 
 
 def bench_config0(args):
@@ -192,11 +197,12 @@ def bench_config0(args):
         with ProcessPoolExecutor(1, mp_context=mp.get_context('spawn')) as ex:
             in_bytes = ex.submit(_config0_write_inputs, inp, shape, block, cell, args.seed).result()
 
-        def step(k, mode, graph_jobs):
+        def step(k, mode, jobs):
             out = os.path.join(d, 'out%d.n5' % k)
-            t = workflow.graph_workflow(inp, 'seg', out, 'graph', block, max_jobs=graph_jobs, mode=mode)
+            t = workflow.graph_workflow(inp, 'seg', out, 'graph', block, max_jobs=jobs['graph'], mode=mode)
             workflow.edge_features_workflow(inp, 'bnd', inp, 'seg', out, 'graph', out, 'features', block,
-                                            max_jobs=1, max_jobs_merge=4, timer=t, mode=mode)
+                                            max_jobs=jobs['features'], max_jobs_merge=jobs['merge'], timer=t,
+                                            mode=mode)
             from cluster_tools_amd import n5
             with n5.File(out, 'r') as f:
                 n_edges = int(f['graph'].attrs['numberOfEdges'])
@@ -206,14 +212,14 @@ def bench_config0(args):
         # a step is a whole workflow run (seconds): at most 1 warm-up + 3 steps
         args.warmup, args.steps = min(args.warmup, 1), max(1, min(args.steps, 3))
 
-        def measure(mode, graph_jobs, base):
+        def measure(mode, jobs, base):
             for k in range(args.warmup):
-                step(base + k, mode, graph_jobs)
+                step(base + k, mode, jobs)
             times, stages, feat_prof = [], {}, {}
             from cluster_tools_amd import ndist
             for k in range(args.steps):
                 t0 = time.perf_counter()
-                st, n_edges = step(base + 100 + k, mode, graph_jobs)
+                st, n_edges = step(base + 100 + k, mode, jobs)
                 times.append(time.perf_counter() - t0)
                 for key, v in st.items():
                     stages[key] = stages.get(key, 0.0) + v / args.steps
@@ -223,8 +229,18 @@ def bench_config0(args):
             return float(np.mean(times)) * 1e3, stages, feat_prof, n_edges
 
         # process mode first: this process has not opened the device yet
-        ms_p, stages_p, _, n_edges = measure('processes', CONFIG0_PROC_JOBS, 0)
-        ms_t, stages_t, feat_prof, _ = measure('threads', 16, 1000)
+        def split():
+            out = {k: {kk: (round(vv, 4) if isinstance(vv, float) else vv) for kk, vv in v.items()
+                       if kk != 'body_profile_of_slowest'} for k, v in workflow.process_stats.items()}
+            out['_block_features_job_profile'] = {
+                k: round(v, 4) for k, v in workflow.process_stats.get('_block_features_job', {}).get(
+                    'body_profile_of_slowest', {}).items()}
+            return out
+        ms_p, stages_p, _, n_edges = measure('processes', CONFIG0_PROC_LAYOUTS['gpu'], 0)
+        proc_split = split()
+        ms_c, stages_c, _, _ = measure('processes', CONFIG0_PROC_LAYOUTS['cpu_layout'], 500)
+        proc_split_c = split()
+        ms_t, stages_t, feat_prof, _ = measure('threads', dict(graph=16, features=1, merge=4), 1000)
 
         from cluster_tools_amd import _lib, n5, rag
         from cluster_tools_amd.blocking import blocking
@@ -283,11 +299,19 @@ def bench_config0(args):
         'data': 'synthetic (jittered-grid Voronoi supervoxels + boundary map) written to gzip N5 (level 1)',
         'config': {'workload': 'BASELINE configs[0]: 125x1250x1250, 64x256x256 blocks (50), GraphWorkflow + '
                                'EdgeFeaturesWorkflow job bodies (harness/workflow.py), every job its own spawned '
-                               'process as LocalTask runs them (%d graph jobs, 1 feature job, 4 merge jobs)'
-                               % CONFIG0_PROC_JOBS,
+                               'process as LocalTask runs them, one job per task (max_jobs 1: a GPU job runs all '
+                               'blocks of its task)',
                    'volume': list(shape), 'block_shape': list(block), 'edges': n_edges,
                    'input_n5_bytes': in_bytes},
         'stage_s': {k: round(v, 4) for k, v in stages_p.items()},
+        'process_split_last_step': proc_split,
+        'process_mode_cpu_layout': {'value': round(V / (ms_c * 1e-3) / 1e9, 4), 'unit': 'Gvoxels/s',
+                                    'ms_per_step': round(ms_c, 2), 'jobs': CONFIG0_PROC_LAYOUTS['cpu_layout'],
+                                    'stage_s': {k: round(v, 4) for k, v in stages_c.items()},
+                                    'process_split_last_step': proc_split_c,
+                                    'what': 'process mode with the job counts of the CPU layout (one graph job '
+                                            'per core): every job process creates and tears down a device '
+                                            'context'},
         'thread_mode': {'value': round(V / (ms_t * 1e-3) / 1e9, 4), 'unit': 'Gvoxels/s', 'ms_per_step': round(ms_t, 2),
                         'stage_s': {k: round(v, 4) for k, v in stages_t.items()},
                         'block_features_split_s': {k: round(v, 4) for k, v in feat_prof.items()},

@@ -460,7 +460,10 @@ def _write_block_features(fo, outKey, pos, shape, chunks, feats, sums, records):
 
 
 # bytes of decoded input (labels + data) staged per ctg_rag_blocks call
-BATCH_BYTES = int(os.environ.get('CTG_BLOCK_BATCH_BYTES', str(2 << 30)))
+# (512 MB: the two page-locked arenas a job pins cost ~0.2 s per GB to pin and
+# again to release at process exit; a one-job process of configs[0] spent 0.94
+# s pinning 2 GB batches, 0.30 s with 512 MB ones, at equal thread-mode time)
+BATCH_BYTES = int(os.environ.get('CTG_BLOCK_BATCH_BYTES', str(512 << 20)))
 
 
 def _batches(items, sizes, limit):

@@ -45,12 +45,23 @@ def _jobs(block_list, n_jobs):
     return [block_list[k::n_jobs] for k in range(n_jobs)]
 
 
-def _proc_main(conn, fn, job):
-    """Body of a job process: run the job, send ('ok', result) or ('err', text)."""
+# per task of the last process-mode run: wall time, slowest job body, and the
+# job processes' (start -> body) and (body end -> exit) times
+process_stats = {}
+
+
+def _proc_main(conn, fn, job, t_spawn):
+    """Body of a job process: run the job, send ('ok', result, timing) or
+    ('err', text).  timing: seconds from the parent's start() to the job
+    body (interpreter, imports), and of the body itself."""
+    t0 = time.time()
     try:
-        conn.send(('ok', fn(job)))
+        res = fn(job)
+        t1 = time.time()
+        conn.send(('ok', res, {'start_s': t0 - t_spawn, 'body_s': t1 - t0, 'end': t1,
+                               'profile': dict(ndist.last_profile)}))
     except BaseException:  # noqa: BLE001 -- reported to the parent, which raises
-        conn.send(('err', traceback.format_exc()))
+        conn.send(('err', traceback.format_exc(), None))
     finally:
         conn.close()
 
@@ -61,26 +72,37 @@ def _run_job_processes(fn, jobs):
     (LocalTask checks each job's log for success, cluster_tasks.py:575-590)."""
     ctx = mp.get_context('spawn')
     procs = []
+    t_task = time.time()
     try:
         for j in jobs:
             r, w = ctx.Pipe(duplex=False)
-            p = ctx.Process(target=_proc_main, args=(w, fn, j), daemon=True)
+            p = ctx.Process(target=_proc_main, args=(w, fn, j, time.time()), daemon=True)
             p.start()
             w.close()
             procs.append((p, r))
-        out, errors = [], []
+        out, errors, timing = [], [], []
         for k, (p, r) in enumerate(procs):
             try:
-                status, val = r.recv()
+                status, val, tm = r.recv()
             except EOFError:
-                status, val = 'err', 'job process exited without a result'
+                status, val, tm = 'err', 'job process exited without a result', None
             p.join()
+            if tm is not None:
+                tm['exit_s'] = time.time() - tm.pop('end')
+                timing.append(tm)
             if status == 'ok' and p.exitcode == 0:
                 out.append(val)
             else:
                 errors.append('job %d (exit code %s): %s' % (k, p.exitcode, val))
         if errors:
             raise RuntimeError('task failed:\n' + '\n'.join(errors))
+        name = getattr(fn, 'func', fn).__name__
+        process_stats[name] = {
+            'jobs': len(jobs), 'task_s': time.time() - t_task,
+            'start_s_max': max((t['start_s'] for t in timing), default=0.0),
+            'body_s_max': max((t['body_s'] for t in timing), default=0.0),
+            'exit_s_max': max((t['exit_s'] for t in timing), default=0.0),
+            'body_profile_of_slowest': max(timing, key=lambda t: t['body_s'])['profile'] if timing else {}}
         return out
     finally:
         for p, r in procs:
