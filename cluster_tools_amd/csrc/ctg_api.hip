@@ -34,9 +34,6 @@ hipError_t bucket_runs(const uint64_t* sorted, int64_t n, int lo_bit, int hi_bit
 hipError_t bucket_sort_pairs(const uint64_t* keys, const uint32_t* vals, uint64_t* ktmp, uint32_t* vtmp,
                              uint64_t* kout, uint32_t* vout, int64_t n, int hi_bit, uint32_t* small, void** temp,
                              size_t* temp_bytes, hipStream_t s);
-hipError_t bucket_sort_pairs2(uint64_t* keys, uint32_t* vals, uint64_t* ktmp, uint32_t* vtmp, uint64_t* kout,
-                              uint32_t* vout, int64_t n, int hi_bit, uint32_t* small, void** temp,
-                              size_t* temp_bytes, uint32_t* l2_scratch, hipStream_t s);
 hipError_t launch_max_pairs(int64_t n, const uint64_t* uv, unsigned long long* out, hipStream_t s);
 hipError_t launch_reduce(int64_t E, const uint32_t* dE, const uint64_t* uniq, const uint32_t* runs,
                          const uint32_t* offs, const uint32_t* perm32, const uint64_t* perm64, int ib,
@@ -270,14 +267,6 @@ static bool bucket_sort_pairs_on(int64_t n) {
     if (e) return e[0] == '1';
     return n <= (int64_t)(32 << 20);
 }
-// Pair sorts above the single-level bucket pass's range (configs[4]'s 1.3e8
-// records): two bucket levels, then the segmented sort on ~500-record segments
-// (ctg_sort.hip bucket_sort_pairs2); CTG_BUCKET_SORT_PAIRS2=0 keeps onesweep.
-static bool bucket_sort_pairs2_on(int64_t n, int key_bits) {
-    const char* e = getenv("CTG_BUCKET_SORT_PAIRS2");
-    if (e) return e[0] == '1' && key_bits > 18;
-    return n > (int64_t)(32 << 20) && key_bits > 18;
-}
 static int64_t sort_wide_digits_max() {
     static const int64_t v = [] {
         const char* e = getenv("CTG_SORT_WIDE_MAX");
@@ -392,14 +381,6 @@ static hipError_t reduce_records(Workspace& w, const ReduceJob& J, hipStream_t s
         // run-length pass / the reduction
         e = bucket_sort_pairs(w.sk_in, w.idx_in, w.uniq, w.keep, w.sk_out, w.idx_out, n, ub + nb, w.bsort, &w.temp,
                               &w.temp_bytes, s);
-        if (e != hipSuccess) return e;
-    } else if (spread && bucket_sort_pairs2_on(n, ub + nb)) {
-        // second-level scratch: 3 x 2^18 + 2 words (stream-ordered pool reuse)
-        uint32_t* l2 = (uint32_t*)dalloc((3 * (4096 * 64) + 2) * sizeof(uint32_t));
-        if (!l2) return hipErrorOutOfMemory;
-        e = bucket_sort_pairs2(w.sk_in, w.idx_in, w.uniq, w.keep, w.sk_out, w.idx_out, n, ub + nb, w.bsort, &w.temp,
-                               &w.temp_bytes, l2, s);
-        dfree(l2);
         if (e != hipSuccess) return e;
     } else if (n <= sort_wide_digits_max()) {
         ROCPRIM_CALL(w, rocprim::radix_sort_pairs<RecordSortConfig>(t, tbytes, w.sk_in, w.sk_out, w.idx_in,

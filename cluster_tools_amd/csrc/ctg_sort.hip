@@ -173,147 +173,6 @@ hipError_t bucket_sort_pairs(const uint64_t* keys, const uint32_t* vals, uint64_
 }
 
 // ---------------------------------------------------------------------------
-// Two bucket levels for large (key, value) sorts (configs[4]: 1.3e8 records).
-// One level of 4096 buckets leaves ~32 K records per bucket, which the
-// segmented sort handles on its slow large-segment path; a second MSD pass
-// splits every first-level bucket by the next L2_BITS key bits, leaving
-// ~500-record segments for the segmented sort's small-segment path.  Each
-// workgroup of the second pass owns one chunk of one first-level bucket (a
-// chunk table built on the device from the bucket counts), so its LDS
-// histogram has only 2^L2_BITS counters.
-// ---------------------------------------------------------------------------
-constexpr int L2_BITS = 6;
-constexpr uint32_t L2_NB = 1u << L2_BITS;
-constexpr int L2_CHUNK = 4096;
-
-// nch[b] = chunks of bucket b (counts[b] / L2_CHUNK, rounded up)
-__global__ __launch_bounds__(256) void k_l2_chunks(const uint32_t* __restrict__ counts, uint32_t nbk,
-                                                   uint32_t* __restrict__ nch) {
-    const uint32_t b = blockIdx.x * 256 + threadIdx.x;
-    if (b < nbk) nch[b] = (counts[b] + L2_CHUNK - 1) / L2_CHUNK;
-}
-
-// this workgroup's (bucket, [start, end)); false past the last chunk
-__device__ __forceinline__ bool l2_chunk(const uint32_t* __restrict__ coff, const uint32_t* __restrict__ offs1,
-                                         uint32_t nbk, uint32_t& b, uint32_t& start, uint32_t& end) {
-    const uint32_t w = blockIdx.x;
-    if (w >= coff[nbk]) return false;
-    uint32_t lo = 0, hi = nbk;   // coff[lo] <= w < coff[hi]
-    while (hi - lo > 1) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (coff[mid] <= w) lo = mid;
-        else hi = mid;
-    }
-    b = lo;
-    start = offs1[b] + (w - coff[b]) * L2_CHUNK;
-    end = min(start + (uint32_t)L2_CHUNK, offs1[b + 1]);
-    return true;
-}
-
-__global__ __launch_bounds__(BK_THREADS) void k_l2_hist(const uint64_t* __restrict__ keys, int shift2,
-                                                        const uint32_t* __restrict__ coff,
-                                                        const uint32_t* __restrict__ offs1, uint32_t nbk,
-                                                        uint32_t* __restrict__ cnt2) {
-    __shared__ uint32_t h[L2_NB];
-    uint32_t b, start, end;
-    if (!l2_chunk(coff, offs1, nbk, b, start, end)) return;
-    for (uint32_t i = threadIdx.x; i < L2_NB; i += BK_THREADS) h[i] = 0;
-    __syncthreads();
-    for (uint32_t i = start + threadIdx.x; i < end; i += BK_THREADS)
-        atomicAdd(&h[(uint32_t)(keys[i] >> shift2) & (L2_NB - 1)], 1u);
-    __syncthreads();
-    for (uint32_t i = threadIdx.x; i < L2_NB; i += BK_THREADS)
-        if (h[i]) atomicAdd(&cnt2[b * L2_NB + i], h[i]);
-}
-
-__global__ __launch_bounds__(BK_THREADS) void k_l2_scatter(const uint64_t* __restrict__ keys,
-                                                           const uint32_t* __restrict__ vals, int shift2,
-                                                           const uint32_t* __restrict__ coff,
-                                                           const uint32_t* __restrict__ offs1, uint32_t nbk,
-                                                           const uint32_t* __restrict__ offs2,
-                                                           uint32_t* __restrict__ cursor2,
-                                                           uint64_t* __restrict__ kout, uint32_t* __restrict__ vout) {
-    constexpr int PER = L2_CHUNK / BK_THREADS;
-    __shared__ uint32_t h[L2_NB];
-    __shared__ uint32_t base[L2_NB];
-    uint32_t b, start, end;
-    if (!l2_chunk(coff, offs1, nbk, b, start, end)) return;
-    for (uint32_t i = threadIdx.x; i < L2_NB; i += BK_THREADS) h[i] = 0;
-    __syncthreads();
-    uint64_t k[PER];
-    uint32_t rank[PER];
-#pragma unroll
-    for (int j = 0; j < PER; ++j) {
-        const uint32_t i = start + j * BK_THREADS + threadIdx.x;
-        k[j] = i < end ? keys[i] : 0ull;
-        rank[j] = i < end ? atomicAdd(&h[(uint32_t)(k[j] >> shift2) & (L2_NB - 1)], 1u) : 0u;
-    }
-    __syncthreads();
-    for (uint32_t i = threadIdx.x; i < L2_NB; i += BK_THREADS)
-        base[i] = h[i] ? offs2[b * L2_NB + i] + atomicAdd(&cursor2[b * L2_NB + i], h[i]) : 0u;
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < PER; ++j) {
-        const uint32_t i = start + j * BK_THREADS + threadIdx.x;
-        if (i < end) {
-            const uint32_t d = base[(uint32_t)(k[j] >> shift2) & (L2_NB - 1)] + rank[j];
-            kout[d] = k[j];
-            vout[d] = vals[i];
-        }
-    }
-}
-
-// (keys, vals) sorted by key bits [0, hi_bit) into (kout, vout) with two
-// bucket levels; keys / vals are overwritten (second-level output), ktmp /
-// vtmp: n each.  Scratch: small (BK_SMALL_WORDS) + 3 x 2^18 + 2 words allocated here.
-hipError_t bucket_sort_pairs2(uint64_t* keys, uint32_t* vals, uint64_t* ktmp, uint32_t* vtmp, uint64_t* kout,
-                              uint32_t* vout, int64_t n, int hi_bit, uint32_t* small, void** temp,
-                              size_t* temp_bytes, uint32_t* l2_scratch, hipStream_t s) {
-    if (n <= 0) return hipSuccess;
-    if (n > 0xFFFFFFFFll || hi_bit > 64 || hi_bit <= BK_MAX_BITS + L2_BITS) return hipErrorInvalidValue;
-    constexpr uint32_t M = 1u << BK_MAX_BITS;
-    const int shift1 = hi_bit - BK_MAX_BITS, shift2 = shift1 - L2_BITS;
-    uint32_t* counts = small;
-    uint32_t* offs1 = small + M;
-    uint32_t* cursor = small + 2 * M + 1;
-    uint32_t* nch = small + 3 * M + 1;      // chunks per bucket
-    uint32_t* coff = small + 4 * M + 2;     // chunk offsets (M + 1)
-    const uint32_t N2 = M * L2_NB;
-    uint32_t* cnt2 = l2_scratch;
-    uint32_t* offs2 = l2_scratch + N2;      // N2 + 1
-    uint32_t* cursor2 = l2_scratch + 2 * N2 + 1;
-    hipError_t e = hipMemsetAsync(counts, 0, M * 4, s);
-    if (e == hipSuccess) e = hipMemsetAsync(cnt2, 0, N2 * 4, s);
-    if (e != hipSuccess) return e;
-    const unsigned nwg = (unsigned)((n + BK_CHUNK - 1) / BK_CHUNK);
-    hipLaunchKernelGGL(k_bucket_hist, dim3(nwg), dim3(BK_THREADS), 0, s, keys, n, shift1, M, counts);
-    hipLaunchKernelGGL(k_bucket_scan, dim3(1), dim3(1024), 0, s, counts, M, offs1, cursor);
-    hipLaunchKernelGGL(k_bucket_scatter_pairs, dim3(nwg), dim3(BK_THREADS), 0, s, keys, vals, n, shift1, M, offs1,
-                       cursor, ktmp, vtmp);
-    hipLaunchKernelGGL(k_l2_chunks, dim3(M / 256), dim3(256), 0, s, counts, M, nch);
-    // chunk offsets; the cursor output of the scan is scratch here (cursor2 is reset by the next scan)
-    hipLaunchKernelGGL(k_bucket_scan, dim3(1), dim3(1024), 0, s, nch, M, coff, cursor2);
-    const unsigned nwg2 = (unsigned)((n + L2_CHUNK - 1) / L2_CHUNK + M);   // >= total chunks
-    hipLaunchKernelGGL(k_l2_hist, dim3(nwg2), dim3(BK_THREADS), 0, s, ktmp, shift2, coff, offs1, M, cnt2);
-    hipLaunchKernelGGL(k_bucket_scan, dim3(1), dim3(1024), 0, s, cnt2, N2, offs2, cursor2);
-    hipLaunchKernelGGL(k_l2_scatter, dim3(nwg2), dim3(BK_THREADS), 0, s, ktmp, vtmp, shift2, coff, offs1, M, offs2,
-                       cursor2, keys, vals);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
-    if (shift2 <= 0) {
-        e = hipMemcpyAsync(kout, keys, (size_t)n * 8, hipMemcpyDeviceToDevice, s);
-        return e != hipSuccess ? e : hipMemcpyAsync(vout, vals, (size_t)n * 4, hipMemcpyDeviceToDevice, s);
-    }
-    size_t need = 0;
-    e = rocprim::segmented_radix_sort_pairs(nullptr, need, keys, kout, vals, vout, (unsigned)n, N2, offs2, offs2 + 1,
-                                            0u, (unsigned)shift2, s);
-    if (e != hipSuccess) return e;
-    ensure(temp, *temp_bytes, need + 256);
-    size_t have = *temp_bytes;
-    return rocprim::segmented_radix_sort_pairs(*temp, have, keys, kout, vals, vout, (unsigned)n, N2, offs2,
-                                               offs2 + 1, 0u, (unsigned)shift2, s);
-}
-
-// ---------------------------------------------------------------------------
 // Runs of equal keys after bucket_sort_keys (the back half's "segment" step):
 // runs never cross buckets, so heads are counted per bucket (one workgroup
 // each), the bucket counts scanned (k_bucket_scan), and every bucket writes

@@ -515,28 +515,3 @@ def test_bucket_sort_skewed_keys(gpu, monkeypatch):
     e_o, f_o = O.boundary_features(lab, bnd)
     np.testing.assert_array_equal(out['edges'], e_o)
     check_features(out['features'], f_o)
-
-
-@pytest.mark.parametrize('skew', [False, True])
-def test_two_level_pair_sort(gpu, monkeypatch, skew):
-    """The two-level bucket sort of (key, slot) pairs (ctg_sort.hip
-    bucket_sort_pairs2, used above 32 M records: configs[4]) forced on a small
-    volume -- with a skewed key set too (background label 0 adjacent to nearly
-    every cell) -- against onesweep and the oracle."""
-    lab, bnd = S.generate((48, 64, 80), cell=4, seed=9)
-    if skew:
-        lab = lab.copy()
-        lab[::3] = 0
-    monkeypatch.setenv('CTG_SORT_PACKED', '0')          # the (key, slot) pair path
-    monkeypatch.setenv('CTG_BUCKET_SORT_PAIRS', '0')    # not the one-level bucket pass
-    monkeypatch.setenv('CTG_BUCKET_SORT_PAIRS2', '1')
-    out = rag.rag_features(lab, bnd)
-    monkeypatch.setenv('CTG_BUCKET_SORT_PAIRS2', '0')   # onesweep
-    ref = rag.rag_features(lab, bnd)
-    np.testing.assert_array_equal(out['edges'], ref['edges'])
-    np.testing.assert_array_equal(out['nodes'], ref['nodes'])
-    np.testing.assert_array_equal(out['features'][:, 9], ref['features'][:, 9])
-    np.testing.assert_allclose(out['features'], ref['features'], rtol=1e-12, atol=1e-15)
-    e_o, f_o = O.boundary_features(lab, bnd)
-    np.testing.assert_array_equal(out['edges'], e_o)
-    check_features(out['features'], f_o)
