@@ -403,6 +403,7 @@ def main():
     scan_ms = []
     narrow_ms = 0.0
     if world > 1:
+        del cdist.host_reads[:]   # device -> host reads of the exchange, counted over the timed steps
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -483,6 +484,8 @@ def main():
             'step_roofline_frac': round(step_bytes / (ms_step * 1e-3) / 1e9 / (HBM_PEAK_GBS * world), 4),
             'phase_ms': {k: round(v, 4) for k, v in timings.items()},
             'records': n_rec, 'direct_faces': n_direct,
+            'exchange_host_reads_per_step': ({k: cdist.host_reads.count(k) / args.steps for k in sorted(set(
+                cdist.host_reads))} if world > 1 else None),
             'cpu_baseline': cpu,
         }
         print(json.dumps(line), flush=True)
