@@ -30,6 +30,10 @@ same three methods, which lets the partition/exchange code run under gloo.
 """
 from __future__ import annotations
 
+import os
+import sys
+import time
+
 import numpy as np
 import torch
 import torch.distributed as dist
@@ -353,11 +357,22 @@ def rag_features_distributed(labels, data=None, offsets=None, own_begin=None, ow
     shape = tuple(labels.shape)
     if world_size_of(group) > 1:
         check_slab_halo(shape, offsets, own_begin, own_end)
+    debug = os.environ.get('CTG_DIST_DEBUG') == '1'   # per-phase wall times on stderr (synchronising)
+    tdbg = [time.perf_counter()]
+
+    def phase(name):
+        if debug:
+            if torch.cuda.is_available():
+                torch.cuda.synchronize()
+            tdbg.append(time.perf_counter())
+            print('[dist r%d] %s %.3f ms' % (dist.get_rank(group), name, (tdbg[-1] - tdbg[-2]) * 1e3),
+                  file=sys.stderr, flush=True)
     backend = backend or HipBackend()
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     keys, sums, recs, nodes, info, _feats = backend.local(labels, data, offsets, own_begin, own_end,
                                                           ignore_label, hist_range)
+    phase('local')
     dev = keys.device
     wire = _wire_device(dev, group)
     n = keys.shape[0]
@@ -390,6 +405,7 @@ def rag_features_distributed(labels, data=None, offsets=None, own_begin=None, ow
     arn = torch.arange(nodes.shape[0], device=dev)
     own_n = (arn >= n_start[rank]) & (arn < n_start[rank] + n_counts[rank])
     own_nodes = torch.where(own_n, nodes, torch.full_like(nodes, NODE_EMPTY))
+    phase('splitters+masks')
 
     key = _plan_key(group, shape, offsets)
     if plan is None:
@@ -402,6 +418,7 @@ def rag_features_distributed(labels, data=None, offsets=None, own_begin=None, ow
                                          plan, rank, group)
         over = over.to(wire)
         dist.all_reduce(over, op=dist.ReduceOp.MAX, group=group)
+        phase('exchange (cap %d rows, %d nodes)' % (plan.cap_rows, plan.cap_nodes))
         if learn:
             # no plan yet: learn the capacities from the true counts now (the
             # only host read before the merge, first call of a shape only)
@@ -413,6 +430,7 @@ def rag_features_distributed(labels, data=None, offsets=None, own_begin=None, ow
         rks, rss, rrs = unpack_rows(rk)
         me, mf = backend.merge(torch.cat([own_keys, rks]), torch.cat([own_sums, rss]),
                                torch.cat([own_recs, rrs]), hist_range)
+        phase('merge (%d rows)' % (own_keys.shape[0] + rks.shape[0]))
         # the result-size read: the merge has returned its size; the overflow
         # flag (all ranks agree on it) comes to the host with it
         ov = _host(over, 'result')
@@ -427,7 +445,9 @@ def rag_features_distributed(labels, data=None, offsets=None, own_begin=None, ow
     # appended so the sorted unique ids always end with exactly one of it
     node_shard = backend.unique(torch.cat([own_nodes, rn, torch.full((1,), NODE_EMPTY, dtype=torch.int64,
                                                                        device=dev)]))[:-1]
+    phase('nodes')
     (e_off, e_tot), (n_off, n_tot) = _exclusive_offsets([n_loc, int(node_shard.shape[0])], group, dev)
+    phase('offsets')
     return DistResult(merged, node_shard, e_off, e_tot, n_off, n_tot, info)
 
 
