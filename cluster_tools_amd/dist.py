@@ -217,8 +217,8 @@ def _uniform_exchange(keys, sums, recs, nodes, e_start, e_counts, n_start, n_cou
 
     Destination d gets a fixed-size segment: [true row count, true node
     count, cap_rows rows of ROW_WORDS int64, cap_nodes node ids].  Empty
-    slots hold key (0, 0) with a zero record (no ADJ bit: the merge drops
-    them) and node id NODE_EMPTY.  Segment layout, gather indices and the overflow flag are
+    slots hold a key (j, j) with a zero record (never an edge, no ADJ bit:
+    the merge drops them) and node id NODE_EMPTY.  Segment layout, gather indices and the overflow flag are
     computed on the device; nothing is read on the host here.
     Returns (received rows, received node ids, overflow flag (device))."""
     world = dist.get_world_size(group)
@@ -236,7 +236,14 @@ def _uniform_exchange(keys, sums, recs, nodes, e_start, e_counts, n_start, n_cou
     else:
         rows = torch.zeros((world * cr, ROW_WORDS), dtype=torch.int64, device=dev)
     ok = ok.reshape(-1, 1)
-    rows = torch.where(ok, rows, torch.zeros_like(rows)).reshape(world, cr * ROW_WORDS)   # empty slot: key (0, 0)
+    # empty slot j: key (j, j) -- never an edge (u == v), and every empty slot
+    # its own run (one shared key made one run of ~world * cap records, which
+    # the merge's one-thread-per-edge reduce walked serially: 16-22 ms)
+    empty = torch.zeros_like(rows)
+    sl = torch.arange(rows.shape[0], device=dev, dtype=torch.int64)
+    empty[:, 0] = sl
+    empty[:, 1] = sl
+    rows = torch.where(ok, rows, empty).reshape(world, cr * ROW_WORDS)
     jn = torch.arange(cn, device=dev)
     nsrc = torch.clamp(n_start.reshape(-1, 1) + jn.reshape(1, -1), max=max(nn - 1, 0)).reshape(-1)
     nok = jn.reshape(1, -1) < n_counts.reshape(-1, 1)
@@ -395,11 +402,11 @@ def rag_features_distributed(labels, data=None, offsets=None, own_begin=None, ow
     e_start = torch.cat([zero, torch.cumsum(e_counts, 0)[:-1]])
     n_start = torch.cat([zero, torch.cumsum(n_counts, 0)[:-1]])
     # this rank's own rows / node ids stay in place; every other one is masked
-    # to an empty slot (SENTINEL-free: key (0, 0) with a zero record is never
-    # an edge, and the merge drops rows without the ADJ bit)
+    # to an empty slot (key (i, i) with a zero record: never an edge, and the
+    # merge drops rows without the ADJ bit)
     ar = torch.arange(n, device=dev)
     own = (ar >= e_start[rank]) & (ar < e_start[rank] + e_counts[rank])
-    own_keys = torch.where(own.reshape(-1, 1), keys, torch.zeros_like(keys))
+    own_keys = torch.where(own.reshape(-1, 1), keys, torch.stack([ar, ar], dim=1))   # (i, i): never an edge
     own_sums = torch.where(own.reshape(-1, 1), sums.reshape(n, 2), torch.zeros_like(sums.reshape(n, 2)))
     own_recs = torch.where(own.reshape(-1, 1), recs.reshape(n, WIDE_WORDS), torch.zeros_like(recs.reshape(n, WIDE_WORDS)))
     arn = torch.arange(nodes.shape[0], device=dev)

@@ -83,7 +83,7 @@ class OracleBackend:
         merged = O.merge_feature_stats([(inv, st)], edges.shape[0], hist_range[0], hist_range[1])
         feats = O.finalize_features(merged, hist_range[0], hist_range[1])
         # ctg_merge_stats keeps only keys with the ADJ bit on some row (need_adj):
-        # the exchange's empty slots (key (0, 0), zero record) disappear here
+        # the exchange's empty slots (keys (j, j), zero records) disappear here
         adj = np.zeros(edges.shape[0], bool)
         np.logical_or.at(adj, inv, (rec[:, 42] & ADJ) != 0)
         return (torch.from_numpy(edges[adj].astype(np.int64)),
