@@ -1086,19 +1086,22 @@ static hipError_t launch_scan_r(const ScanParams& P, const RecordBuf& R, Counter
     if (nwg <= 0) return hipSuccess;
     if (nwg > 0x7FFFFFFF) return hipErrorInvalidValue;
     dim3 grid((unsigned)nwg);
+    // diagnostic: unused dynamic LDS per workgroup (CTG_SCAN_LDS_PAD bytes) lowers
+    // the workgroups resident per CU -- the scan's sensitivity to occupancy
+    static const unsigned pad = [] { const char* v = getenv("CTG_SCAN_LDS_PAD"); return v ? (unsigned)atoi(v) : 0u; }();
     if (P.blocks) {
         if (P.fast40)
-            hipLaunchKernelGGL((k_face_scan<LabelT, DataT, MODE, true, true, NR>), grid, dim3(SCAN_THREADS), 0, s, Q, R,
-                               C);
-        else
-            hipLaunchKernelGGL((k_face_scan<LabelT, DataT, MODE, false, true, NR>), grid, dim3(SCAN_THREADS), 0, s, Q,
+            hipLaunchKernelGGL((k_face_scan<LabelT, DataT, MODE, true, true, NR>), grid, dim3(SCAN_THREADS), pad, s, Q,
                                R, C);
+        else
+            hipLaunchKernelGGL((k_face_scan<LabelT, DataT, MODE, false, true, NR>), grid, dim3(SCAN_THREADS), pad, s,
+                               Q, R, C);
     } else if (P.fast40) {
-        hipLaunchKernelGGL((k_face_scan<LabelT, DataT, MODE, true, false, NR>), grid, dim3(SCAN_THREADS), 0, s, Q, R,
-                           C);
+        hipLaunchKernelGGL((k_face_scan<LabelT, DataT, MODE, true, false, NR>), grid, dim3(SCAN_THREADS), pad, s, Q,
+                           R, C);
     } else {
-        hipLaunchKernelGGL((k_face_scan<LabelT, DataT, MODE, false, false, NR>), grid, dim3(SCAN_THREADS), 0, s, Q, R,
-                           C);
+        hipLaunchKernelGGL((k_face_scan<LabelT, DataT, MODE, false, false, NR>), grid, dim3(SCAN_THREADS), pad, s, Q,
+                           R, C);
     }
     return hipGetLastError();
 }
