@@ -723,6 +723,7 @@ static int scan_records(Workspace& w, const ScanParams& P, int64_t V, hipStream_
     for (int attempt = 0; attempt < 4; ++attempt) {
         CTG_CHECK(ensure_records(w, need, 0));
         CTG_CHECK(hipMemsetAsync(w.counters, 0, sizeof(Counters), s));
+        ev.mark(0);   // (re-recorded here: the scan phase brackets the scan launch alone)
         CTG_CHECK(launch_face_scan(P, w.rec, w.counters, s));
         ev.mark(1);
         CTG_CHECK(hipMemcpyAsync(w.counters_host, w.counters, sizeof(Counters), hipMemcpyDeviceToHost, s));
