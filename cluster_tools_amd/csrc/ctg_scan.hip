@@ -468,21 +468,36 @@ __device__ __forceinline__ double dpp_f64(double v) {
 #ifndef CTG_PAIR_FOLD
 #define CTG_PAIR_FOLD 1
 #endif
-template <bool FAST40, typename StageT, int NPER>
-__device__ __forceinline__ void fold_boundary_grouped(Table& T, const StageT (&e)[NPER], const int (&slot)[NPER],
-                                                      const uint32_t (&pv)[NPER], int lane, RecordBuf R, Counters* C,
-                                                      double scale, double offset) {
+#ifndef CTG_PAIR_FOLD_AFF
+#define CTG_PAIR_FOLD_AFF 1
+#endif
+template <int MODE, bool FAST40, bool BATCH, typename StageT, int NPER>
+__device__ __forceinline__ void fold_grouped(Table& T, const StageT (&e)[NPER], const int (&slot)[NPER],
+                                             const uint32_t (&pv)[NPER], int lane, RecordBuf R, Counters* C,
+                                             double scale, double offset) {
+    constexpr bool BND = MODE == MODE_BOUNDARY;
+    constexpr bool AFF = MODE == MODE_AFFINITY;
 #pragma unroll
     for (int i = 0; i < NPER; ++i) {
         const int sl = slot[i];
         if (sl == -1) {   // table full: a direct record, no grouping (rare)
             bool dummy = false;
-            fold_stats<MODE_BOUNDARY, FAST40, false, StageT>(T, e[i], -1, PIV_EMPTY, R, C, scale, offset, dummy, 0);
+            fold_stats<MODE, FAST40, BATCH, StageT>(T, e[i], -1, PIV_EMPTY, R, C, scale, offset, dummy, 0);
         }
-        const bool v = sl >= 0;
-        const float a = __uint_as_float(e[i].z), b = __uint_as_float(e[i].w);
+        // adjacency-only entries (fold_stats' rule): the flag, no samples, no group
+        const bool adj = (AFF || BATCH) && e[i].w == MARK_ADJ && (AFF || e[i].z == MARK_ADJ);
+        if (sl >= 0 && adj) atomicOr(&T.w[sl][21], ADJ_FLAG);
+        const bool v = sl >= 0 && !adj;
+        // affinity entries carry one sample (.w a marker) or two (.w the second)
+        const bool two = BND || (AFF && e[i].w < MARK_ONE_ADJ);
+        const float a = __uint_as_float(e[i].z);
+        const float b = two ? __uint_as_float(e[i].w) : a;
         const double da = (double)a, db = (double)b;
-        if (v) hist_add2(T, sl, sample_slot<FAST40>(da, scale, offset), sample_slot<FAST40>(db, scale, offset));
+        if (v) {
+            const int sa = sample_slot<FAST40>(da, scale, offset);
+            if (two) hist_add2(T, sl, sa, sample_slot<FAST40>(db, scale, offset));
+            else atomicAdd(&T.w[sl][sa >> 1], 1u << ((sa & 1) * 16));
+        }
         // the entry's pivot: the first sample that claims the empty word (CAS)
         uint32_t p = pv[i];
         if (v && p == PIV_EMPTY) {
@@ -491,20 +506,23 @@ __device__ __forceinline__ void fold_boundary_grouped(Table& T, const StageT (&e
             p = old == PIV_EMPTY ? mine : old;
         }
         const double dp = (double)__uint_as_float(p);
-        const double ea = da - dp, eb = db - dp;
+        const double ea = da - dp, eb = two ? db - dp : 0.0;
         double sm = ea + eb, sq = ea * ea + eb * eb;
         uint32_t mn = f2ord(fminf(a, b)), mx = f2ord(fmaxf(a, b));
+        // a nearest-neighbour sample proves adjacency (long-range calls with the Bloom filter)
+        uint32_t nnf = (AFF && v && e[i].w == MARK_ONE_ADJ) ? 1u : 0u;
         // groups: every lane active here (no divergent branch encloses this);
         // a lane without a slot gets a key no other lane has
         const uint32_t key = v ? (uint32_t)sl : 0x80000000u | (uint32_t)lane;
         const bool g1 = dpp_x1(key) == key;
         {
             const double s1 = dpp_f64<1>(sm), q1 = dpp_f64<1>(sq);
-            const uint32_t mn1 = dpp_x1(mn), mx1 = dpp_x1(mx);
+            const uint32_t mn1 = dpp_x1(mn), mx1 = dpp_x1(mx), f1 = AFF ? dpp_x1(nnf) : 0u;
             sm = g1 ? sm + s1 : sm;
             sq = g1 ? sq + q1 : sq;
             mn = g1 ? min(mn, mn1) : mn;
             mx = g1 ? max(mx, mx1) : mx;
+            nnf = g1 ? nnf | f1 : nnf;
         }
         // both exchanges unconditional: under a short-circuit && the compiler
         // runs a DPP with part of the wave masked off, and a masked source
@@ -513,16 +531,18 @@ __device__ __forceinline__ void fold_boundary_grouped(Table& T, const StageT (&e
         const bool g2 = g1 & (g1_x2 != 0u) & (key_x2 == key);
         {
             const double s2 = dpp_f64<2>(sm), q2 = dpp_f64<2>(sq);
-            const uint32_t mn2 = dpp_x2(mn), mx2 = dpp_x2(mx);
+            const uint32_t mn2 = dpp_x2(mn), mx2 = dpp_x2(mx), f2 = AFF ? dpp_x2(nnf) : 0u;
             sm = g2 ? sm + s2 : sm;
             sq = g2 ? sq + q2 : sq;
             mn = g2 ? min(mn, mn2) : mn;
             mx = g2 ? max(mx, mx2) : mx;
+            nnf = g2 ? nnf | f2 : nnf;
         }
         const bool lead = !(g1 && (lane & 1)) && !(g2 && (lane & 2));
         if (v && lead) {
             atomicMin(&T.w[sl][22], mn);
             atomicMax(&T.w[sl][23], mx);
+            if (AFF && nnf) atomicOr(&T.w[sl][21], ADJ_FLAG);
             atomicAdd(&T.sum[sl], sm);
             atomicAdd(&T.sq[sl], sq);
         }
@@ -591,8 +611,10 @@ __device__ __forceinline__ void fold_batch(Table& T, const StageT* __restrict__ 
             pv[i] = __hip_atomic_load(&T.w[slot[i]][24], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
 #if CTG_PAIR_FOLD
-    if constexpr (MODE == MODE_BOUNDARY && !BATCH) {
-        fold_boundary_grouped<FAST40, StageT, NPER>(T, e, slot, pv, lane, R, C, scale, offset);
+    // grouped atomics: whole-array boundary maps (CTG_PAIR_FOLD 1) and, A/B,
+    // affinity maps (CTG_PAIR_FOLD_AFF)
+    if constexpr ((MODE == MODE_BOUNDARY || (CTG_PAIR_FOLD_AFF && MODE == MODE_AFFINITY)) && !BATCH) {
+        fold_grouped<MODE, FAST40, BATCH, StageT, NPER>(T, e, slot, pv, lane, R, C, scale, offset);
         return;
     }
 #endif
