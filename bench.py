@@ -206,9 +206,13 @@ def bench_config0(args):
             from cluster_tools_amd import n5
             with n5.File(out, 'r') as f:
                 n_edges = int(f['graph'].attrs['numberOfEdges'])
+            for key in ('s0/sub_features', 's0/sub_features_stats', 'features', 's0/sub_graphs'):
+                p = os.path.join(out, key)
+                out_bytes[key] = sum(os.path.getsize(os.path.join(r, fn)) for r, _, fs in os.walk(p) for fn in fs)
             shutil.rmtree(out)
             return t.stages, n_edges
 
+        out_bytes = {}   # on-disk bytes of the outputs (last step)
         # a step is a whole workflow run (seconds): at most 1 warm-up + 3 steps
         args.warmup, args.steps = min(args.warmup, 1), max(1, min(args.steps, 3))
 
@@ -302,7 +306,8 @@ def bench_config0(args):
                                'process as LocalTask runs them, one job per task (max_jobs 1: a GPU job runs all '
                                'blocks of its task)',
                    'volume': list(shape), 'block_shape': list(block), 'edges': n_edges,
-                   'input_n5_bytes': in_bytes},
+                   'input_n5_bytes': in_bytes, 'output_bytes': out_bytes,
+                   'stats_compression': os.environ.get('CTG_STATS_COMPRESSION', 'raw')},
         'stage_s': {k: round(v, 4) for k, v in stages_p.items()},
         'process_split_last_step': proc_split,
         'process_mode_cpu_layout': {'value': round(V / (ms_c * 1e-3) / 1e9, 4), 'unit': 'Gvoxels/s',
