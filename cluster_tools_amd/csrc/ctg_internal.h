@@ -21,7 +21,13 @@ constexpr int WAVE = 64;
 constexpr int SCAN_THREADS = CTG_SCAN_THREADS;   // 8 waves per workgroup (1024: 16 waves, one per CU)
 constexpr int TILE_X = 64;             // one wave row
 constexpr int TILE_Y = 8;
-constexpr int TABLE_CAP = SCAN_THREADS;   // LDS edge-table entries (power of two; one per thread in a flush)
+// LDS edge-table entries: a multiple of 4 (4-slot buckets), at most one per
+// thread in a flush; a power of two or not (the home bucket is a multiply-high)
+#ifndef CTG_TABLE_CAP
+#define CTG_TABLE_CAP SCAN_THREADS
+#endif
+constexpr int TABLE_CAP = CTG_TABLE_CAP;
+static_assert(TABLE_CAP % 4 == 0 && TABLE_CAP <= SCAN_THREADS, "table capacity");
 constexpr int NBINS = 40;              // vigra UserRangeHistogram<40> (nifty default)
 constexpr int NSLOTS = NBINS + 2;      // left outliers, 40 bins, right outliers
 constexpr int HWORDS = 21;             // 42 u16 slots packed in 21 u32 words

@@ -99,7 +99,7 @@ struct __align__(16) Table {
     // first sample, claimed by CAS); odd row stride (25 words) so atomics to
     // different entries spread over the LDS banks
     uint32_t w[TABLE_CAP][NREC_WORDS + 1];
-    uint16_t compact[TABLE_CAP];
+    uint16_t compact[(TABLE_CAP + WAVE - 1) / WAVE * WAVE];   // per-wave flush ranks
     uint32_t wave_cnt[WAVES];
     uint32_t used;
     uint32_t flush_req;   // a wave asked for a flush; every wave joins at its next poll
@@ -131,16 +131,22 @@ __device__ __forceinline__ uint32_t pivot_bits(float a) { return a == a ? __floa
 #ifndef CTG_HASH24
 #define CTG_HASH24 1
 #endif
+constexpr bool TABLE_POW2 = (TABLE_CAP & (TABLE_CAP - 1)) == 0;
+// hash -> first slot of a 4-slot bucket (any table size: multiply-high)
+__device__ __forceinline__ uint32_t bucket_of(uint32_t h) {
+    if constexpr (TABLE_POW2) return h & (TABLE_CAP - 4);
+    else return __umulhi(h, (uint32_t)(TABLE_CAP / 4)) * 4u;
+}
 __device__ __forceinline__ uint32_t home_bucket(uint32_t u, uint32_t v) {
 #if CTG_HASH24
     const uint32_t p = (u & 0xFFFFFFu) * 0x9E3779u + ((v ^ (u >> 24)) & 0xFFFFFFu) * 0x85EBCBu;
-    return (p >> 12) & (TABLE_CAP - 4);
+    return TABLE_POW2 ? bucket_of(p >> 12) : bucket_of(p << 8);
 #else
     uint32_t h = u * 0x9E3779B1u + v * 0x85EBCA6Bu;
     h ^= h >> 15;
     h *= 0x2C1B3C6Du;
     h ^= h >> 13;
-    return h & (TABLE_CAP - 4);
+    return bucket_of(h);
 #endif
 }
 
@@ -164,7 +170,6 @@ __device__ __forceinline__ void lds_barrier() {
 // drop.)
 template <int MODE>
 __device__ __noinline__ void table_flush_waves(Table& T, RecordBuf R, Counters* C) {
-    static_assert(TABLE_CAP == SCAN_THREADS, "one table entry per thread in the flush");
     lds_barrier();
     const int tid = threadIdx.x;
     const int lane = tid & (WAVE - 1), wv = tid >> 6;
@@ -172,7 +177,8 @@ __device__ __noinline__ void table_flush_waves(Table& T, RecordBuf R, Counters* 
         T.used = 0;
         T.flush_req = 0;
     }
-    const uint64_t k = T.key[tid];
+    // entry tid (threads past TABLE_CAP own none)
+    const uint64_t k = tid < TABLE_CAP ? T.key[tid] : EMPTY_KEY;
     const bool out = k != EMPTY_KEY;
     const uint64_t m = __ballot(out);
     if (m) {
@@ -320,7 +326,7 @@ __device__ __noinline__ int table_insert(Table& T, uint32_t h, int empty, uint64
 #pragma unroll 1
     for (int i = 0; i <= CTG_PROBE_BUCKETS;) {
         if (j0 >= 4) {
-            b = (b + 4) & (TABLE_CAP - 1);
+            b = TABLE_POW2 ? ((b + 4) & (TABLE_CAP - 1)) : (b + 4 >= (uint32_t)TABLE_CAP ? 0u : b + 4);
             j0 = 0;
             ++i;
             continue;
@@ -468,8 +474,11 @@ __device__ __forceinline__ double dpp_f64(double v) {
 #ifndef CTG_PAIR_FOLD
 #define CTG_PAIR_FOLD 1
 #endif
+// affinity maps: off -- measured slower (configs[3] 12-channel scan 45.8 ->
+// 49.9 ms, 3-channel 8.98 -> 9.84 ms): the channel loop's entries rarely
+// share a slot within a quad, and the exchanges lengthen every fold
 #ifndef CTG_PAIR_FOLD_AFF
-#define CTG_PAIR_FOLD_AFF 1
+#define CTG_PAIR_FOLD_AFF 0
 #endif
 template <int MODE, bool FAST40, bool BATCH, typename StageT, int NPER>
 __device__ __forceinline__ void fold_grouped(Table& T, const StageT (&e)[NPER], const int (&slot)[NPER],
@@ -645,7 +654,10 @@ __device__ __forceinline__ uint32_t shl1(uint32_t v, uint32_t edge) {
 #define FLUSH_TABLE table_flush_waves
 
 template <typename LabelT, typename DataT, int MODE, bool FAST40, bool BATCH, int ROWS>
-__global__ __launch_bounds__(SCAN_THREADS, 4) void k_face_scan(ScanParams P, RecordBuf R, Counters* C) {
+#ifndef CTG_SCAN_MIN_WAVES
+#define CTG_SCAN_MIN_WAVES 4   // waves per SIMD the register budget must allow
+#endif
+__global__ __launch_bounds__(SCAN_THREADS, CTG_SCAN_MIN_WAVES) void k_face_scan(ScanParams P, RecordBuf R, Counters* C) {
     constexpr bool BND = MODE == MODE_BOUNDARY;
     constexpr bool AFF = MODE == MODE_AFFINITY;
     constexpr bool STATS = MODE != MODE_GRAPH;

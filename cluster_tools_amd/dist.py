@@ -190,13 +190,20 @@ class ExchangePlan:
     notices it at the result-size read (the overflow flag rides along) and
     redoes the exchange with capacities learned from that call."""
 
-    def __init__(self, cap_rows=0, cap_nodes=0):
+    def __init__(self, cap_rows=0, cap_nodes=0, cap_own=None):
         self.cap_rows = int(cap_rows)
         self.cap_nodes = int(cap_nodes)
+        # own rows merged with the received ones (this rank's; no collective
+        # depends on it): None until the first call of the shape sizes it
+        self.cap_own = cap_own
+
+    @staticmethod
+    def grow(x):
+        return int(x) + int(x) // 2 + 64
 
     @staticmethod
     def from_counts(max_rows, max_nodes):
-        return ExchangePlan(max_rows + max_rows // 2 + 64, max_nodes + max_nodes // 2 + 64)
+        return ExchangePlan(ExchangePlan.grow(max_rows), ExchangePlan.grow(max_nodes))
 
 
 _plans = {}
@@ -377,7 +384,7 @@ def rag_features_distributed(labels, data=None, offsets=None, own_begin=None, ow
     backend = backend or HipBackend()
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
-    keys, sums, recs, nodes, info, _feats = backend.local(labels, data, offsets, own_begin, own_end,
+    keys, sums, recs, nodes, info, feats = backend.local(labels, data, offsets, own_begin, own_end,
                                                           ignore_label, hist_range)
     phase('local')
     dev = keys.device
@@ -401,17 +408,13 @@ def rag_features_distributed(labels, data=None, offsets=None, own_begin=None, ow
     zero = torch.zeros(1, dtype=torch.int64, device=dev)
     e_start = torch.cat([zero, torch.cumsum(e_counts, 0)[:-1]])
     n_start = torch.cat([zero, torch.cumsum(n_counts, 0)[:-1]])
-    # this rank's own rows / node ids stay in place; every other one is masked
-    # to an empty slot (key (i, i) with a zero record: never an edge, and the
-    # merge drops rows without the ADJ bit)
-    ar = torch.arange(n, device=dev)
-    own = (ar >= e_start[rank]) & (ar < e_start[rank] + e_counts[rank])
-    own_keys = torch.where(own.reshape(-1, 1), keys, torch.stack([ar, ar], dim=1))   # (i, i): never an edge
-    own_sums = torch.where(own.reshape(-1, 1), sums.reshape(n, 2), torch.zeros_like(sums.reshape(n, 2)))
-    own_recs = torch.where(own.reshape(-1, 1), recs.reshape(n, WIDE_WORDS), torch.zeros_like(recs.reshape(n, WIDE_WORDS)))
+    # this rank's own node ids stay in place; every other one is masked to an
+    # empty slot (its rows were sent; its node ids travel with them)
     arn = torch.arange(nodes.shape[0], device=dev)
     own_n = (arn >= n_start[rank]) & (arn < n_start[rank] + n_counts[rank])
     own_nodes = torch.where(own_n, nodes, torch.full_like(nodes, NODE_EMPTY))
+    own_lo = e_start[rank]
+    own_hi = own_lo + e_counts[rank]
     phase('splitters+masks')
 
     key = _plan_key(group, shape, offsets)
@@ -435,18 +438,69 @@ def rag_features_distributed(labels, data=None, offsets=None, own_begin=None, ow
             if int(ov[0]):
                 continue
         rks, rss, rrs = unpack_rows(rk)
-        me, mf = backend.merge(torch.cat([own_keys, rks]), torch.cat([own_sums, rss]),
-                               torch.cat([own_recs, rrs]), hist_range)
-        phase('merge (%d rows)' % (own_keys.shape[0] + rks.shape[0]))
-        # the result-size read: the merge has returned its size; the overflow
-        # flag (all ranks agree on it) comes to the host with it
-        ov = _host(over, 'result')
+        # Own rows that can share a key with a received row: the received keys'
+        # u values lie in this rank's range, and the own rows are sorted by u,
+        # so they are the slice [lo, hi) of own rows with u between the
+        # smallest and the largest received u.  Only that slice is merged with
+        # the received rows; every other own row keeps the local call's
+        # features.  (Empty slots are keyed (j, j).)
+        real = rks[:, 0] != rks[:, 1]
+        ru = _ordered(rks[:, 0])
+        big = torch.iinfo(torch.int64).max
+        umin = torch.where(real, ru, torch.full_like(ru, big)).min().reshape(1) if ru.numel() else \
+            torch.full((1,), big, dtype=torch.int64, device=dev)
+        umax = torch.where(real, ru, torch.full_like(ru, -big - 1)).max().reshape(1) if ru.numel() else \
+            torch.full((1,), -big - 1, dtype=torch.int64, device=dev)
+        lo = torch.searchsorted(ou.contiguous(), umin, right=False) if n else torch.zeros(1, dtype=torch.int64,
+                                                                                           device=dev)
+        hi = torch.searchsorted(ou.contiguous(), umax, right=True) if n else torch.zeros(1, dtype=torch.int64,
+                                                                                          device=dev)
+        lo = torch.clamp(torch.minimum(lo, own_hi), min=own_lo)
+        hi = torch.maximum(torch.minimum(hi, own_hi), lo)
+        while True:
+            if plan.cap_own is None:   # first call of the shape: size the slice (this rank only)
+                plan.cap_own = ExchangePlan.grow(int(_host(hi - lo, 'plan')[0]))
+            c2 = plan.cap_own
+            j = torch.arange(c2, device=dev, dtype=torch.int64)
+            ok2 = (lo + j) < hi
+            src = torch.clamp(lo + j, max=max(n - 1, 0))
+            slot_key = torch.stack([j, j], dim=1) + (1 << 40)   # empty: (j, j), apart from the received slots' j
+            k2 = torch.where(ok2.reshape(-1, 1), keys.index_select(0, src), slot_key) if n else slot_key
+            s2 = torch.where(ok2.reshape(-1, 1), sums.reshape(n, 2).index_select(0, src),
+                             torch.zeros((c2, 2), dtype=sums.dtype, device=dev)) if n else \
+                torch.zeros((c2, 2), dtype=torch.float64, device=dev)
+            r2 = torch.where(ok2.reshape(-1, 1), recs.reshape(n, WIDE_WORDS).index_select(0, src),
+                             torch.zeros((c2, WIDE_WORDS), dtype=recs.dtype, device=dev)) if n else \
+                torch.zeros((c2, WIDE_WORDS), dtype=torch.int32, device=dev)
+            me, mf = backend.merge(torch.cat([k2, rks]), torch.cat([s2, rss]), torch.cat([r2, rrs]), hist_range)
+            phase('merge (%d + %d rows)' % (c2, rks.shape[0]))
+            # the result-size read: the merge has returned its size; the
+            # overflow flags (the exchange's agreed by all ranks) and the slice
+            # bounds come to the host with it
+            ov = _host(torch.cat([over.to(dev), (hi - lo > c2).to(torch.int64).reshape(1), lo, hi,
+                                  own_lo.reshape(1), own_hi.reshape(1)]), 'result')
+            if int(ov[0]) or not int(ov[3]):
+                break
+            plan.cap_own = ExchangePlan.grow(int(ov[5] - ov[4]))   # this rank's slice only: no collective
         if int(ov[0]):
+            cap_own = plan.cap_own
             plan = ExchangePlan.from_counts(int(ov[1]), int(ov[2]))
+            plan.cap_own = cap_own
             continue
         break
     _plans[key] = plan
-    merged = {'edges': _tensor(me, keys), 'features': _tensor(mf, keys)}
+    lo_i, hi_i, olo, ohi = (int(x) for x in ov[4:8])
+    me, mf = _tensor(me, keys), _tensor(mf, keys)
+    loc_e = [keys[olo:lo_i], keys[hi_i:ohi]]
+    loc_f = [feats[olo:lo_i], feats[hi_i:ohi]]
+    if offsets is not None:
+        # affinity partials keep non-adjacent pairs: a local-only key is an
+        # edge when one of its samples proved adjacency (ADJ bit of its record)
+        adj = [recs[olo:lo_i, 42] < 0, recs[hi_i:ohi, 42] < 0]
+        loc_e = [x[m] for x, m in zip(loc_e, adj)]
+        loc_f = [x[m] for x, m in zip(loc_f, adj)]
+    # sorted by construction: own rows below the slice, the merged slice, own rows above it
+    merged = {'edges': torch.cat([loc_e[0], me, loc_e[1]]), 'features': torch.cat([loc_f[0], mf, loc_f[1]])}
     n_loc = int(merged['edges'].shape[0])
     # nodes went to the same ranges in the all_to_all; one NODE_EMPTY is
     # appended so the sorted unique ids always end with exactly one of it

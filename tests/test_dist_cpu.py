@@ -171,9 +171,10 @@ def test_device_splitters_match_numpy_restatement():
 
 
 def _plan_worker(rank, world, port, outdir):
-    """Three calls on the same slab: the first learns the ExchangePlan, the
+    """Four calls on the same slab: the first learns the ExchangePlan, the
     second reuses it (no host read before the result-size read), the third
-    starts from a plan too small for its counts (overflow -> regrow -> redo)."""
+    starts from exchange capacities too small for its counts (overflow ->
+    regrow -> redo), the fourth from a too small merge slice (redone locally)."""
     import torch.distributed as dist
     from tests.dist_helpers import OracleBackend
     os.environ['MASTER_ADDR'] = '127.0.0.1'
@@ -186,7 +187,7 @@ def _plan_worker(rank, world, port, outdir):
     sl = slice(z0[rank] - halo, z0[rank + 1])
     args = (np.ascontiguousarray(lab[sl]), np.ascontiguousarray(bnd[sl]))
     outs, reads = [], []
-    for call, plan in enumerate([None, None, cdist.ExchangePlan(1, 1)]):
+    for call, plan in enumerate([None, None, cdist.ExchangePlan(1, 1), cdist.ExchangePlan(1 << 16, 1 << 16, 1)]):
         del cdist.host_reads[:]
         res = cdist.rag_features_distributed(*args, own_begin=(halo, 0, 0), backend=OracleBackend(), plan=plan)
         reads.append(list(cdist.host_reads))
@@ -204,6 +205,11 @@ def test_exchange_plan_reuse_and_overflow(tmp_path, world):
     for r in range(world):
         reads = list(np.load(tmp_path / ('reads%d.npy' % r)))
         # (the shard offsets are read after the result size)
-        assert reads[0] == 'plan|result|offsets'           # first call of the shape: learns its plan
+        assert reads[0] == 'plan|plan|result|offsets'      # first call of the shape: learns its capacities
         assert reads[1] == 'result|offsets'                # plan reused: nothing read before the result size
-        assert reads[2] == 'result|result|offsets'         # too small: overflow seen with the result, redone
+        # exchange capacity too small: overflow seen with the result, exchange redone
+        # (the merge slice sized on the truncated exchange may need a local redo too)
+        assert reads[2].startswith('plan|result|result') and reads[2].endswith('|offsets')
+        assert 'plan' not in reads[2][5:]
+        # merge-slice capacity too small: this rank redoes its merge alone (no collective)
+        assert reads[3].startswith('result|') and reads[3].endswith('|offsets')
