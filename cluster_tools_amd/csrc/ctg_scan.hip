@@ -67,7 +67,12 @@ constexpr int AFF_G = CTG_AFF_G;
 #define CTG_NPER 2
 #endif
 constexpr int NPER = CTG_NPER;                            // staged entries folded per lane
-constexpr int STAGE_CAP = WAVE * NPER;                    // stage entries per wave
+// the narrow-tile boundary kernel (configs[4]'s fragmented volumes) folds one
+// staged entry per lane: its scan 15.3 -> 14.5 ms, records +5 %, step -1.5 %
+// (A/B of CTG_NPER=1 builds); every other kernel keeps NPER
+#ifndef CTG_NPER_NARROW
+#define CTG_NPER_NARROW 1
+#endif
 // u16 histogram slots: a table entry holds at most 65535 samples.  Each wave
 // folds at most this many samples between two table flushes (it requests a
 // flush before a batch would exceed it), so no entry can pass the bound.
@@ -663,6 +668,9 @@ __global__ __launch_bounds__(SCAN_THREADS, CTG_SCAN_MIN_WAVES) void k_face_scan(
     constexpr bool STATS = MODE != MODE_GRAPH;
     using StageT = typename std::conditional<STATS, uint4, uint2>::type;
     __shared__ Table T;
+    constexpr int NP = (ROWS == ROWS_NARROW && ROWS_NARROW != ROWS_WIDE && MODE == MODE_BOUNDARY && !BATCH)
+                           ? CTG_NPER_NARROW : NPER;   // staged entries folded per lane
+    constexpr int STAGE_CAP = WAVE * NP;               // stage entries per wave
     __shared__ StageT stage_all[WAVES][STAGE_CAP];
     if constexpr (!BATCH) {
         // narrow_rows == 2: both tile widths are launched back to back and the
@@ -866,7 +874,7 @@ __global__ __launch_bounds__(SCAN_THREADS, CTG_SCAN_MIN_WAVES) void k_face_scan(
                 wsamp += add;
             }
             const uint64_t t0 = stamps ? stamp_now() : 0;
-            fold_batch<MODE, FAST40, BATCH, StageT, NPER>(T, stage, nbuf, lane, R, C, scale, offset, need, ablate);
+            fold_batch<MODE, FAST40, BATCH, StageT, NP>(T, stage, nbuf, lane, R, C, scale, offset, need, ablate);
             nbuf = 0;
             if (stamps) t_fold += stamp_now() - t0;
 #if CTG_POLL_AFTER_FOLD
