@@ -18,6 +18,9 @@
 
 #include <algorithm>
 #include <atomic>
+#include <condition_variable>
+#include <deque>
+#include <functional>
 #include <cerrno>
 #include <cstdint>
 #include <cstdio>
@@ -448,6 +451,84 @@ ChunkPtr get_chunk(const std::string& path, int format, int ndim, const int64_t*
     return c;
 }
 
+// ---------------------------------------------------------------------------
+// Readahead: a job that walks its blocks in C order (one per call: the
+// reference's per-block API, initial_sub_graphs.py:146-157) decodes each
+// block's chunks only when its call arrives, a few chunks at a time.  After
+// every box read, the chunk box that follows it in C order (same extent) is
+// queued for decode into the cache on a small background pool, so the next
+// call finds its chunks inflated.  CTG_IO_READAHEAD=0 disables it.
+// ---------------------------------------------------------------------------
+class Prefetcher {
+public:
+    static Prefetcher& get() {   // function-local: destroyed before the cache globals
+        static Prefetcher p;
+        return p;
+    }
+    void submit(std::function<void()> f) {
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            if (stop_ || q_.size() >= kMaxQueued) return;   // never unbounded: drop the hint
+            q_.push_back(std::move(f));
+            if (th_.empty())
+                for (int i = 0; i < kThreads; ++i) th_.emplace_back([this] { run(); });
+        }
+        cv_.notify_one();
+    }
+    ~Prefetcher() {
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            stop_ = true;
+            q_.clear();
+        }
+        cv_.notify_all();
+        for (auto& t : th_) t.join();
+    }
+
+private:
+    static constexpr int kThreads = 8;
+    static constexpr size_t kMaxQueued = 64;
+    void run() {
+        while (true) {
+            std::function<void()> f;
+            {
+                std::unique_lock<std::mutex> lk(mu_);
+                cv_.wait(lk, [this] { return stop_ || !q_.empty(); });
+                if (stop_) return;
+                f = std::move(q_.front());
+                q_.pop_front();
+            }
+            f();
+        }
+    }
+    std::mutex mu_;
+    std::condition_variable cv_;
+    std::deque<std::function<void()>> q_;
+    std::vector<std::thread> th_;
+    bool stop_ = false;
+};
+
+bool readahead_on() {
+    static const bool on = [] {
+        const char* e = getenv("CTG_IO_READAHEAD");
+        return !(e && e[0] == '0');
+    }();
+    return on && cache_budget() > 0;
+}
+
+// chunk box [c0, c0 + nc) -> the box after it in C order (last axis first;
+// false past the grid's end)
+bool next_chunk_box(int ndim, const int64_t* grid, int64_t* c0, const int64_t* nc) {
+    for (int a = ndim - 1; a >= 0; --a) {
+        if (c0[a] + nc[a] < grid[a]) {
+            c0[a] += nc[a];
+            for (int b = a + 1; b < ndim; ++b) c0[b] = 0;
+            return true;
+        }
+    }
+    return false;
+}
+
 int check_geometry(int ndim, const int64_t* shape, const int64_t* chunks, int dtype_size) {
     if (ndim < 1 || ndim > MAXD || dtype_size < 1 || dtype_size > 16) return -1;
     for (int a = 0; a < ndim; ++a)
@@ -549,6 +630,35 @@ int ctg_io_read_box(const char* ds_path, int format, int dtype_size, int big_end
             if (a < 0) break;
         }
     });
+    if (err.msg.empty() && readahead_on()) {
+        int64_t grid[MAXD], nxt[MAXD], cnt[MAXD];
+        for (int a = 0; a < ndim; ++a) {
+            grid[a] = (shape[a] + chunks[a] - 1) / chunks[a];
+            nxt[a] = c0[a];
+            cnt[a] = nc[a];
+        }
+        if (next_chunk_box(ndim, grid, nxt, cnt)) {
+            const std::string ds(ds_path);
+            std::vector<int64_t> ch(chunks, chunks + ndim);
+            for (int64_t ci = 0; ci < n_chunks; ++ci) {
+                int64_t pos[MAXD];
+                int64_t r = ci;
+                bool inside = true;
+                for (int a = ndim - 1; a >= 0; --a) {
+                    pos[a] = nxt[a] + r % cnt[a];
+                    r /= cnt[a];
+                    inside = inside && pos[a] < grid[a];
+                }
+                if (!inside) continue;
+                std::string path = chunk_path(ds.c_str(), format, ndim, pos);
+                Prefetcher::get().submit([path, format, ndim, ch, es, swap, compression] {
+                    bool missing = false;
+                    std::string msg;
+                    get_chunk(path, format, ndim, ch.data(), es, swap, compression, &missing, &msg);
+                });
+            }
+        }
+    }
     if (!err.msg.empty()) {
         ctg::set_error(err.msg);
         return CTG_ERR_ARG;
