@@ -59,7 +59,7 @@ WORKLOADS = {
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument('--gpus', type=int, default=1)
-    p.add_argument('--steps', type=int, default=10)
+    p.add_argument('--steps', type=int, default=20)
     p.add_argument('--warmup', type=int, default=3)
     p.add_argument('--config', default='1', choices=sorted(WORKLOADS))
     p.add_argument('--size', type=int, default=None, help='cube edge (voxels; per GPU for weak scaling)')
