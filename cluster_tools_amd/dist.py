@@ -464,7 +464,9 @@ def rag_features_distributed(labels, data=None, offsets=None, own_begin=None, ow
             j = torch.arange(c2, device=dev, dtype=torch.int64)
             ok2 = (lo + j) < hi
             src = torch.clamp(lo + j, max=max(n - 1, 0))
-            slot_key = torch.stack([j, j], dim=1) + (1 << 40)   # empty: (j, j), apart from the received slots' j
+            # empty slot: (j, j) -- never an edge; small j keeps every key below 2^32 (a larger one
+            # sends ctg_merge_stats down its dense-relabel path); equal empty keys only merge empty runs
+            slot_key = torch.stack([j, j], dim=1)
             k2 = torch.where(ok2.reshape(-1, 1), keys.index_select(0, src), slot_key) if n else slot_key
             s2 = torch.where(ok2.reshape(-1, 1), sums.reshape(n, 2).index_select(0, src),
                              torch.zeros((c2, 2), dtype=sums.dtype, device=dev)) if n else \
