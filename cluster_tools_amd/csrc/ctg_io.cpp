@@ -190,13 +190,39 @@ bool deflate_all(const unsigned char* src, size_t n, int level, bool gzip, std::
     return rc == Z_STREAM_END;
 }
 
+// copy n_el elements of es bytes, byte-swapped (N5 payloads are big-endian);
+// word-wise bswap for the 2 / 4 / 8-byte types (the compiler vectorises these
+// loops), bytes otherwise
 inline void swap_copy(unsigned char* dst, const unsigned char* src, size_t n_el, int es, bool swap) {
     if (!swap || es == 1) {
         std::memcpy(dst, src, n_el * es);
         return;
     }
-    for (size_t i = 0; i < n_el; ++i)
-        for (int b = 0; b < es; ++b) dst[i * es + b] = src[i * es + es - 1 - b];
+    if (es == 8) {
+        for (size_t i = 0; i < n_el; ++i) {
+            uint64_t v;
+            std::memcpy(&v, src + 8 * i, 8);
+            v = __builtin_bswap64(v);
+            std::memcpy(dst + 8 * i, &v, 8);
+        }
+    } else if (es == 4) {
+        for (size_t i = 0; i < n_el; ++i) {
+            uint32_t v;
+            std::memcpy(&v, src + 4 * i, 4);
+            v = __builtin_bswap32(v);
+            std::memcpy(dst + 4 * i, &v, 4);
+        }
+    } else if (es == 2) {
+        for (size_t i = 0; i < n_el; ++i) {
+            uint16_t v;
+            std::memcpy(&v, src + 2 * i, 2);
+            v = __builtin_bswap16(v);
+            std::memcpy(dst + 2 * i, &v, 2);
+        }
+    } else {
+        for (size_t i = 0; i < n_el; ++i)
+            for (int b = 0; b < es; ++b) dst[i * es + b] = src[i * es + es - 1 - b];
+    }
 }
 
 uint16_t be16(const unsigned char* p) { return (uint16_t)((p[0] << 8) | p[1]); }

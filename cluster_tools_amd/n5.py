@@ -310,8 +310,12 @@ class Dataset:
             if counts[i] < 0:
                 res.append(None)
                 continue
-            buf = (ctypes.c_char * (int(counts[i]) * dt.itemsize)).from_address(outs[i]) if counts[i] else b''
-            res.append(np.frombuffer(bytes(buf), dtype=dt).copy() if counts[i] else np.zeros(0, dt))
+            if counts[i]:
+                # one copy out of the native buffer (a bytes() round trip would make two)
+                buf = (ctypes.c_char * (int(counts[i]) * dt.itemsize)).from_address(outs[i])
+                res.append(np.frombuffer(buf, dtype=dt).copy())
+            else:
+                res.append(np.zeros(0, dt))
             lib.ctg_io_free(outs[i])
         return res
 
