@@ -515,3 +515,31 @@ def test_harness_job_processes_order_and_failure():
         workflow._run_jobs(_square_job, [2, -1], 'processes')
     with pytest.raises(ValueError):
         workflow._run_jobs(_square_job, [1], 'fibers')
+
+
+@pytest.mark.parametrize('dtype', ['uint8', 'int16', 'uint16', 'float32', 'uint32', 'float64', 'uint64', 'int64'])
+def test_native_codec_byte_swaps_every_width(tmp_path, monkeypatch, dtype):
+    """N5 payloads are big-endian: the native codec's word-wise swaps (2 / 4 /
+    8 bytes) agree with numpy's '>' dtypes, for box reads, varlen chunks and
+    raw / gzip payloads."""
+    _with_codec(monkeypatch, True)
+    rng = np.random.default_rng(11)
+    info = np.iinfo(dtype) if np.dtype(dtype).kind in 'iu' else None
+    data = (rng.integers(info.min, info.max, (9, 20, 17), dtype=dtype, endpoint=True) if info is not None
+            else rng.standard_normal((9, 20, 17)).astype(dtype))
+    for comp in ('raw', 'gzip'):
+        p = str(tmp_path / ('%s_%s.n5' % (dtype, comp)))
+        with n5.File(p) as f:
+            ds = f.create_dataset('d', shape=data.shape, chunks=(4, 8, 8), dtype=dtype, compression=comp)
+            ds[:] = data                                        # native aligned writer
+            np.testing.assert_array_equal(ds[:], data)          # native box reader
+            np.testing.assert_array_equal(ds[1:8, 3:19, 2:15], data[1:8, 3:19, 2:15])
+            with open(os.path.join(p, 'd', '0', '0', '0'), 'rb') as fh:
+                buf = fh.read()[4 + 4 * 3:]
+            raw = zlib.decompress(buf, 16 + zlib.MAX_WBITS) if comp == 'gzip' else buf
+            np.testing.assert_array_equal(np.frombuffer(raw, dtype=np.dtype(dtype).newbyteorder('>')).reshape(4, 8, 8),
+                                          data[:4, :8, :8])
+            flat = data.ravel()[:1000]
+            ds.write_chunks([(0, 0, 1)], [flat], varlen=True)   # varlen chunk, native writer and reader
+            np.testing.assert_array_equal(ds.read_chunks([(0, 0, 1)])[0], flat)
+    n5._native().ctg_io_cache_clear()
