@@ -515,20 +515,23 @@ def _block_features(graphPath, subgraphKey, dataPath, dataKey, labelsPath, label
     per_voxel = 8 + max(1, n_ch) * data_dtype.itemsize
     batches = _batches(list(range(len(geo))), [v * per_voxel for v in vox], BATCH_BYTES)
     max_vox = max(sum(vox[i] for i in bt) for bt in batches)
-    arenas = [(rag.host_arena(max_vox * 8), rag.host_arena(max_vox * max(1, n_ch) * data_dtype.itemsize))
-              for _ in range(min(2, len(batches)))]
+    # the first arena pair now; the second (double buffering) is pinned by the
+    # reader thread while batch 0 runs on the GPU (pinning costs ~0.2 s/GB,
+    # a large share of a short-lived job process)
+    arena_bytes = (max_vox * 8, max_vox * max(1, n_ch) * data_dtype.itemsize)
+    arenas = [(rag.host_arena(arena_bytes[0]), rag.host_arena(arena_bytes[1]))]
     _prof('setup', t)
     try:
-        _block_batches(batches, arenas, geo, vox, n_ch, data_dtype, dataPath, dataKey, labelsPath, labelsKey,
-                       outPath, outKey, shape, chunks, offsets, ignore)
+        _block_batches(batches, arenas, arena_bytes, geo, vox, n_ch, data_dtype, dataPath, dataKey, labelsPath,
+                       labelsKey, outPath, outKey, shape, chunks, offsets, ignore)
     finally:
         for pair in arenas:
             for a in pair:
                 rag.release_arena(a)
 
 
-def _block_batches(batches, arenas, geo, vox, n_ch, data_dtype, dataPath, dataKey, labelsPath, labelsKey,  # noqa: N803
-                   outPath, outKey, shape, chunks, offsets, ignore):  # noqa: N803
+def _block_batches(batches, arenas, arena_bytes, geo, vox, n_ch, data_dtype, dataPath, dataKey, labelsPath,  # noqa: N803
+                   labelsKey, outPath, outKey, shape, chunks, offsets, ignore):  # noqa: N803
 
     with _open(dataPath, 'r') as fd, _open(labelsPath, 'r') as fl, _open(outPath) as fo:
         ds_data, ds_lab = fd[dataKey], fl[labelsKey]
@@ -538,6 +541,8 @@ def _block_batches(batches, arenas, geo, vox, n_ch, data_dtype, dataPath, dataKe
         def load(k):
             """decode batch k into arena k % 2 -> (label arena, data arena, descriptors)"""
             t0 = time.perf_counter()
+            if k % 2 == len(arenas):
+                arenas.append((rag.host_arena(arena_bytes[0]), rag.host_arena(arena_bytes[1])))
             la, da = arenas[k % 2]
             descs, reads, lo_, do_ = [], [], 0, 0
             for i in batches[k]:
