@@ -123,14 +123,22 @@ def computeMergeableRegionGraph(labelsPath, labelsKey, roiBegin, roiEnd, graphPa
     roiEnd = [int(e) for e in roiEnd]
     begin = [max(b - 1, 0) for b in roiBegin] if increaseRoi else list(roiBegin)
     shape = [e - b for b, e in zip(begin, roiEnd)]
-    labels = np.empty(shape, dtype=np.uint64)
-    with _open(labelsPath, 'r') as f:
-        _read_into(f[labelsKey], list(zip(begin, roiEnd)), labels)
-    t = _prof('read', t)
-    own = ([b - o for b, o in zip(roiBegin, begin)], [e - o for e, o in zip(roiEnd, begin)])
-    res = rag.rag_blocks_arena(labels.reshape(-1), [dict(label_offset=0, shape=shape, own=own,
-                                                         graph=([0, 0, 0], shape))],
-                               ignore_label=bool(ignoreLabel))[0]
+    # decoded straight into a page-locked arena from the process pool: a job
+    # calls this once per block, and a fresh pageable ROI would be faulted in
+    # and staged by the runtime's pageable copy on every call
+    nvox = int(np.prod(shape))
+    arena = rag.host_arena(nvox * 8)
+    try:
+        labels = arena.view(np.uint64, nvox).reshape(shape)
+        with _open(labelsPath, 'r') as f:
+            _read_into(f[labelsKey], list(zip(begin, roiEnd)), labels)
+        t = _prof('read', t)
+        own = ([b - o for b, o in zip(roiBegin, begin)], [e - o for e, o in zip(roiEnd, begin)])
+        res = rag.rag_blocks_arena(labels.reshape(-1), [dict(label_offset=0, shape=shape, own=own,
+                                                             graph=([0, 0, 0], shape))],
+                                   ignore_label=bool(ignoreLabel))[0]
+    finally:
+        rag.release_arena(arena)
     t = _prof('compute', t)
     with _open(graphPath) as f:
         g = f[subgraphKey]
