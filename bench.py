@@ -74,6 +74,9 @@ def parse():
     # exchange over gloo (the driver's multi-GPU runs use the defaults: RCCL,
     # device = LOCAL_RANK)
     p.add_argument('--backend', default='nccl', choices=['nccl', 'gloo'])
+    p.add_argument('--dist-path', action='store_true',
+                   help='run the multi-GPU step (cluster_tools_amd/dist.py: splitters, all_to_all exchange, merge) '
+                        'even at WORLD_SIZE 1 -- an RCCL rehearsal on a one-GPU box (launch under torch.distributed.run)')
     p.add_argument('--device', type=int, default=None)
     return p.parse_args()
 
@@ -350,9 +353,10 @@ def main():
     local = int(os.environ.get('LOCAL_RANK', '0'))
     if args.gpus != world and world > 1:
         print('warning: --gpus %d but WORLD_SIZE %d' % (args.gpus, world), file=sys.stderr)
+    use_dist = world > 1 or args.dist_path
     dev = local if args.device is None else args.device
     torch.cuda.set_device(dev)
-    if world > 1:
+    if use_dist:
         if args.backend == 'nccl':
             dist.init_process_group('nccl', device_id=torch.device('cuda', dev))
         else:
@@ -392,7 +396,7 @@ def main():
         bnd = None
     torch.cuda.synchronize()
 
-    if world > 1:
+    if use_dist:
         from cluster_tools_amd import dist as cdist
         step_fn = lambda: cdist.rag_features_distributed(lab, data, offsets=offsets, own_begin=own)  # noqa: E731
     else:
@@ -407,7 +411,7 @@ def main():
     rag.set_profiling(True)
     scan_ms = []
     narrow_ms = 0.0
-    if world > 1:
+    if use_dist:
         del cdist.host_reads[:]   # device -> host reads of the exchange, counted over the timed steps
         dist.barrier()
     torch.cuda.synchronize()
@@ -422,12 +426,12 @@ def main():
         scan_ms.append(tm['scan'] + tm.get('narrow', 0.0))
         narrow_ms = tm.get('narrow', 0.0)
     torch.cuda.synchronize()
-    if world > 1:
+    if use_dist:
         dist.barrier()
     t1 = time.perf_counter()
     rag.set_profiling(False)
     elapsed = t1 - t0
-    if world > 1:
+    if use_dist:
         tt = torch.tensor([elapsed], dtype=torch.float64, device='cuda' if args.backend == 'nccl' else 'cpu')
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
@@ -440,7 +444,7 @@ def main():
     ms_step = elapsed / args.steps * 1e3
     value = total_vox / (elapsed / args.steps) / 1e9
     n_edges = n_edges_local
-    if world > 1:
+    if use_dist:
         te = torch.tensor([n_edges_local], dtype=torch.int64, device='cuda' if args.backend == 'nccl' else 'cpu')
         dist.all_reduce(te)
         n_edges = int(te.item())
@@ -479,7 +483,8 @@ def main():
             'dtype': 'u64 labels / f32 samples / f64 stats',
             'data': 'synthetic (jittered-grid Voronoi supervoxels + boundary map, generated in HBM)',
             'config': {'workload': label % (S, cell),
-                       'volume': list(gshape), 'edges': n_edges, 'parallelism': 'z-slab x%d' % world},
+                       'volume': list(gshape), 'edges': n_edges, 'parallelism': 'z-slab x%d' % world,
+                       'step': 'dist.rag_features_distributed (%s)' % args.backend if use_dist else 'rag_features'},
             'roofline': {'bound': 'hbm', 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                          'frac': round(achieved / HBM_PEAK_GBS, 4),
                          'traffic': traffic,
@@ -490,12 +495,12 @@ def main():
             'phase_ms': {k: round(v, 4) for k, v in timings.items()},
             'records': n_rec, 'direct_faces': n_direct,
             'exchange_host_reads_per_step': ({k: cdist.host_reads.count(k) / args.steps for k in sorted(set(
-                cdist.host_reads))} if world > 1 else None),
+                cdist.host_reads))} if use_dist else None),
             'cpu_baseline': cpu,
         }
         print(json.dumps(line), flush=True)
     res.free()
-    if world > 1:
+    if use_dist:
         dist.destroy_process_group()
 
 

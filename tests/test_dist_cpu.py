@@ -66,6 +66,7 @@ def _worker(rank, world, port, shape, cell, outdir, ignore_label, big=False):
 
 
 @pytest.mark.parametrize('world,shape,cell,ignore,big', [
+    (1, (20, 24, 22), 5, False, False),   # the exchange with itself (bench.py --dist-path at N=1)
     (2, (24, 40, 36), 6, False, False),
     (3, (30, 33, 29), 5, True, False),
     (2, (20, 30, 28), 5, False, True),

@@ -70,3 +70,46 @@ def test_two_rank_slabs_equal_whole_volume(tmp_path, affinity):
     o = [np.load(tmp_path / ('o%d.npy' % r)) for r in range(world)]
     assert o[0][0] == 0 and o[1][0] == len(np.load(tmp_path / 'e0.npy'))
     assert o[0][1] == o[1][1] == ref['edges'].shape[0]
+
+
+def _rccl_worker(rank, world, port, outdir, affinity):
+    """One rank over RCCL ("nccl"): the exchange's collectives (all_gather of
+    the splitter samples, the uniform all_to_all_single, the overflow
+    all_reduce, the shard-size all_gather) run on HBM tensors through RCCL --
+    the code path the driver's 8-GPU scaling run takes, at world 1."""
+    import torch.distributed as dist
+    from cluster_tools_amd import dist as cdist
+    from cluster_tools_amd import rag
+    from cluster_tools_amd import synthetic
+    torch.cuda.set_device(0)
+    dist.init_process_group('nccl', init_method='tcp://127.0.0.1:%d' % port, rank=rank, world_size=world,
+                            device_id=torch.device('cuda', 0))
+    assert cdist._wire_device(torch.device('cuda', 0), None).type == 'cuda'
+    offs = synthetic.NN_OFFSETS if affinity else None
+    lab, bnd = rag.synth_volume(SHAPE, cell=7, seed=9)
+    data = rag.synth_affinities(bnd, offs) if affinity else bnd
+    for _ in range(2):   # the second call reuses the learned ExchangePlan
+        del cdist.host_reads[:]
+        res = cdist.rag_features_distributed(lab, data, offsets=offs, own_begin=(0, 0, 0))
+    np.save(os.path.join(outdir, 'e.npy'), res.edges())
+    np.save(os.path.join(outdir, 'f.npy'), res.features())
+    np.save(os.path.join(outdir, 'n.npy'), res.node_shard.cpu().numpy())
+    np.save(os.path.join(outdir, 'reads.npy'), np.array(list(cdist.host_reads)))
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize('affinity', [False, True])
+def test_rccl_world1_exchange_equals_single_call(tmp_path, affinity):
+    from cluster_tools_amd import rag
+    from cluster_tools_amd import synthetic
+    mp.spawn(_rccl_worker, args=(1, _free_port(), str(tmp_path), affinity), nprocs=1, join=True)
+    lab, bnd = rag.synth_volume(SHAPE, cell=7, seed=9)
+    offs = synthetic.NN_OFFSETS if affinity else None
+    data = rag.synth_affinities(bnd, offs) if affinity else bnd
+    ref = rag.rag_features(lab.cpu().numpy().view(np.uint64), data.cpu().numpy(), offsets=offs)
+    np.testing.assert_array_equal(np.load(tmp_path / 'e.npy'), ref['edges'])
+    np.testing.assert_allclose(np.load(tmp_path / 'f.npy'), ref['features'], rtol=1e-9, atol=1e-12)
+    np.testing.assert_array_equal(np.load(tmp_path / 'n.npy').astype(np.uint64), ref['nodes'])
+    # plan reused: no host read before the result size
+    assert list(np.load(tmp_path / 'reads.npy')) == ['result', 'offsets']
