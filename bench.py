@@ -372,16 +372,17 @@ def main():
     if aff and world > 1:
         raise SystemExit('affinity workloads are single-GPU lines (--gpus 1)')
     if scaling == 'weak':
-        Zr = S                                 # owned planes per rank
-        gshape = (S * world, S, S)
+        gshape = (S * world, S, S)             # S owned planes per rank
     else:
         if S % world:
             raise SystemExit('--size must be divisible by the number of ranks')
-        Zr = S // world
         gshape = (S, S, S)
-    halo = 1 if rank > 0 else 0
-    # rank r owns z in [r*Zr, (r+1)*Zr) and reads the plane below as halo
-    lab, bnd = rag.synth_volume((Zr + halo, S, S), cell=cell, seed=args.seed, z_offset=rank * Zr - halo,
+    # rank r owns z in [r*Zr, (r+1)*Zr) and reads the plane(s) below as halo:
+    # the slab plan of the C ABI (ctg_mgpu_slab)
+    from cluster_tools_amd.dist import slab_plan
+    z_read, z_own, z_end = slab_plan(gshape[0], world, rank)
+    Zr, halo = z_end - z_own, z_own - z_read
+    lab, bnd = rag.synth_volume((Zr + halo, S, S), cell=cell, seed=args.seed, z_offset=z_read,
                                 global_shape=gshape)
     own = (halo, 0, 0)
     offsets = None

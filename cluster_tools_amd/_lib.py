@@ -63,6 +63,7 @@ PROTOTYPES = {
     'ctg_unique_labels': (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, ctypes.c_int, c_vp, ctypes.POINTER(c_vp)]),
     'ctg_merge_stats': (ctypes.c_int, [c_vp, c_vp, c_vp, ctypes.c_int64, ctypes.c_double, ctypes.c_double,
                                        ctypes.c_int, ctypes.c_int, c_vp, ctypes.POINTER(c_vp)]),
+    'ctg_mgpu_slab': (ctypes.c_int, [ctypes.c_int64, ctypes.c_int, ctypes.c_int, c_vp, ctypes.c_int, c_vp]),
     'ctg_merge_feature_rows': (ctypes.c_int, [c_vp, c_vp, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, c_vp,
                                               ctypes.c_int, c_vp]),
     'ctg_unique_pairs': (ctypes.c_int, [c_vp, ctypes.c_int64, ctypes.c_int, c_vp, ctypes.POINTER(c_vp)]),

@@ -31,6 +31,8 @@ hipError_t bucket_sort_keys(const uint64_t* keys, uint64_t* tmp, uint64_t* out, 
                             uint32_t* small, void** temp, size_t* temp_bytes, hipStream_t s);
 hipError_t bucket_runs(const uint64_t* sorted, int64_t n, int lo_bit, int hi_bit, uint32_t* small, uint64_t* uniq,
                        uint32_t* runs, uint32_t* roffs, uint32_t* dE, hipStream_t s);
+hipError_t sorted_runs(const uint64_t* sorted, int64_t n, int ib, uint32_t* small, uint64_t* uniq, uint32_t* runs,
+                       uint32_t* roffs, uint32_t* dE, hipStream_t s);
 hipError_t bucket_sort_pairs(const uint64_t* keys, const uint32_t* vals, uint64_t* ktmp, uint32_t* vtmp,
                              uint64_t* kout, uint32_t* vout, int64_t n, int hi_bit, uint32_t* small, void** temp,
                              size_t* temp_bytes, hipStream_t s);
@@ -267,6 +269,13 @@ static bool bucket_sort_pairs_on(int64_t n) {
     if (e) return e[0] == '1';
     return n <= (int64_t)(32 << 20);
 }
+// runs of the onesweep-sorted keys by sorted_runs (ctg_sort.hip: count, scan,
+// write) instead of rocPRIM's run_length_encode + exclusive_scan;
+// CTG_SORTED_RUNS=0 restores the library pair for A/B
+static bool sorted_runs_on() {
+    const char* e = getenv("CTG_SORTED_RUNS");   // read per call: tests switch it
+    return !(e && e[0] == '0');
+}
 static int64_t sort_wide_digits_max() {
     static const int64_t v = [] {
         const char* e = getenv("CTG_SORT_WIDE_MAX");
@@ -374,8 +383,14 @@ static hipError_t reduce_records(Workspace& w, const ReduceJob& J, hipStream_t s
         ROCPRIM_CALL(w, rocprim::radix_sort_keys<RecordSortConfig>(t, tbytes, w.sk_in, w.sk_out, (size_t)n,
                                                                    (unsigned)ib, (unsigned)(ib + ub + nb), s));
         ev.mark(3);
-        auto key_only = rocprim::make_transform_iterator(w.sk_out, [ib] __device__(uint64_t k) { return k >> ib; });
-        ROCPRIM_CALL(w, rocprim::run_length_encode(t, tbytes, key_only, (unsigned)n, w.uniq, w.runs, dE_all, s));
+        if (sorted_runs_on()) {
+            e = sorted_runs(w.sk_out, n, ib, w.bsort, w.uniq, w.runs, w.offs, dE_all, s);
+            if (e != hipSuccess) return e;
+            have_offs = true;
+        } else {
+            auto key_only = rocprim::make_transform_iterator(w.sk_out, [ib] __device__(uint64_t k) { return k >> ib; });
+            ROCPRIM_CALL(w, rocprim::run_length_encode(t, tbytes, key_only, (unsigned)n, w.uniq, w.runs, dE_all, s));
+        }
     } else if (spread && bucket_sort_pairs_on(n)) {
         // tmp buffers: w.uniq (keys) and w.keep (values) are free until the
         // run-length pass / the reduction
@@ -391,7 +406,13 @@ static hipError_t reduce_records(Workspace& w, const ReduceJob& J, hipStream_t s
     }
     if (!packed) {
         ev.mark(3);
-        ROCPRIM_CALL(w, rocprim::run_length_encode(t, tbytes, w.sk_out, (unsigned)n, w.uniq, w.runs, dE_all, s));
+        if (sorted_runs_on()) {
+            e = sorted_runs(w.sk_out, n, 0, w.bsort, w.uniq, w.runs, w.offs, dE_all, s);
+            if (e != hipSuccess) return e;
+            have_offs = true;
+        } else {
+            ROCPRIM_CALL(w, rocprim::run_length_encode(t, tbytes, w.sk_out, (unsigned)n, w.uniq, w.runs, dE_all, s));
+        }
     }
     // offsets over the n-bound: entries past E_all are never read
     if (!have_offs)
@@ -530,6 +551,32 @@ extern "C" {
 int ctg_version(void) { return 1; }
 
 const char* ctg_last_error(void) { return g_err.c_str(); }
+
+int ctg_mgpu_slab(int64_t Z, int world_size, int rank, const int64_t* offsets, int n_channels, int64_t* out) {
+    if (Z <= 0 || world_size <= 0 || rank < 0 || rank >= world_size || !out || n_channels < 0 ||
+        (n_channels > 0 && !offsets)) {
+        set_error("ctg_mgpu_slab: invalid arguments");
+        return CTG_ERR_ARG;
+    }
+    if (world_size > Z) {
+        set_error("ctg_mgpu_slab: more ranks than z planes");
+        return CTG_ERR_ARG;
+    }
+    int64_t down = 1, up = 0;   // planes a face / partner reaches below and above a voxel
+    for (int c = 0; c < n_channels; ++c) {
+        down = std::max<int64_t>(down, -offsets[3 * c]);
+        up = std::max<int64_t>(up, offsets[3 * c]);
+    }
+    if (up > 0 && world_size > 1) {
+        set_error("ctg_mgpu_slab: positive z offsets need an upper halo, which the z-slab layout does not have");
+        return CTG_ERR_UNSUPPORTED;
+    }
+    const int64_t z0 = Z * rank / world_size, z1 = Z * (rank + 1) / world_size;
+    out[0] = z0 - std::min(down, z0);
+    out[1] = z0;
+    out[2] = z1;
+    return CTG_OK;
+}
 
 int ctg_device_count(int* count) {
     CTG_CHECK(hipGetDeviceCount(count));

@@ -325,6 +325,23 @@ def _exclusive_offsets(n_locals, group, device):
     return [(sum(row[k] for row in allc[:r]), sum(row[k] for row in allc)) for k in range(len(n_locals))]
 
 
+def slab_plan(Z, world, rank, offsets=None):
+    """(read_begin, own_begin, own_end) z planes of rank ``rank`` of ``world``
+    over a volume of ``Z`` planes: ``ctg_mgpu_slab`` (include/ctg.h) -- owned
+    planes [Z*r/W, Z*(r+1)/W), read from as many halo planes below as the faces
+    / offsets reach down.  ``own_begin[0]`` of the local call is
+    ``own_begin - read_begin``."""
+    from . import _lib
+    import ctypes
+    off = None if offsets is None else np.ascontiguousarray(np.asarray(offsets, dtype=np.int64).reshape(-1, 3))
+    out = np.zeros(3, dtype=np.int64)
+    _lib.check(_lib.load().ctg_mgpu_slab(int(Z), int(world), int(rank),
+                                         None if off is None else off.ctypes.data_as(ctypes.c_void_p),
+                                         0 if off is None else int(off.shape[0]),
+                                         out.ctypes.data_as(ctypes.c_void_p)), 'ctg_mgpu_slab')
+    return int(out[0]), int(out[1]), int(out[2])
+
+
 def check_slab_halo(shape, offsets, own_begin, own_end):
     """The slab layout gives every rank the planes below its owned range as a
     lower halo and nothing above it.  An affinity sample aff[c, p] needs the

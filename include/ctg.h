@@ -160,6 +160,21 @@ int ctg_merge_stats(const uint64_t* keys, const double* sums, const uint32_t* re
                     int64_t n, double hist_lo, double hist_hi, int keep_stats,
                     int mem, void* stream, ctg_result** out);
 
+/* Multi-GPU z-slab plan (SURVEY §8(b) ctg_mgpu_*; replaces the reference's
+ * block-grid job split, graph/initial_sub_graphs.py:110-129 with
+ * utils/volume_utils.py blocks_in_volume, for one rank per GPU): rank `rank` of
+ * `world_size` owns planes [out[1], out[2]) = [Z*rank/W, Z*(rank+1)/W) of a
+ * volume of Z planes and reads [out[0], out[2]): below its owned range as many
+ * halo planes as the face / offsets reach down (1 for boundary maps and
+ * nearest-neighbour affinities, max(-o_z) for long-range offsets), none for
+ * rank 0.  ctg_rag_features' own_begin[0] is out[1] - out[0].  The ranks'
+ * partial tables (keep_stats) are combined after the exchange by
+ * ctg_merge_stats; the exchange itself runs over RCCL in the host layer
+ * (cluster_tools_amd/dist.py).  Positive z offsets (a partner above the slab)
+ * with world_size > 1 are CTG_ERR_UNSUPPORTED: the z-slab layout has no upper
+ * halo.  Host-only: needs no device. */
+int ctg_mgpu_slab(int64_t Z, int world_size, int rank, const int64_t* offsets, int n_channels, int64_t* out);
+
 /* Merge reference-layout feature rows (n x 10 float64, [mean, var, min,
  * q10..q90, max, count]) of global edges ids[i] in [id_begin, id_end) into
  * out ((id_end - id_begin) x 10): count sum, count-weighted mean, exact pooled

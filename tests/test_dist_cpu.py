@@ -214,3 +214,26 @@ def test_exchange_plan_reuse_and_overflow(tmp_path, world):
         assert 'plan' not in reads[2][5:]
         # merge-slice capacity too small: this rank redoes its merge alone (no collective)
         assert reads[3].startswith('result|') and reads[3].endswith('|offsets')
+
+
+def test_mgpu_slab_plan_c_abi():
+    """ctg_mgpu_slab (include/ctg.h; host-only, no device): owned ranges tile
+    [0, Z) in rank order, the halo below reaches as far as the faces / offsets
+    (1 plane for boundary maps, max(-o_z) for long-range offsets, none on rank
+    0), and positive z offsets are refused when the volume is split."""
+    from cluster_tools_amd import _lib
+    from cluster_tools_amd import synthetic as S
+    for Z, world in [(1024, 1), (2048, 8), (101, 4), (7, 7)]:
+        for offs, down in [(None, 1), (S.NN_OFFSETS, 1), (S.LR_OFFSETS, 4)]:
+            plans = [cdist.slab_plan(Z, world, r, offs) for r in range(world)]
+            assert plans[0][:2] == (0, 0) and plans[-1][2] == Z
+            for r, (rd, own, end) in enumerate(plans):
+                assert own == Z * r // world and end == Z * (r + 1) // world and end > own
+                assert own - rd == (min(down, own) if r else 0)
+    with pytest.raises(_lib.CtgError, match='upper halo'):
+        cdist.slab_plan(64, 2, 0, [[1, 0, 0]])
+    assert cdist.slab_plan(64, 1, 0, [[1, 0, 0]]) == (0, 0, 64)
+    with pytest.raises(_lib.CtgError):
+        cdist.slab_plan(4, 8, 0)
+    with pytest.raises(_lib.CtgError):
+        cdist.slab_plan(64, 2, 2)
