@@ -270,11 +270,12 @@ static bool bucket_sort_pairs_on(int64_t n) {
     return n <= (int64_t)(32 << 20);
 }
 // runs of the onesweep-sorted keys by sorted_runs (ctg_sort.hip: count, scan,
-// write) instead of rocPRIM's run_length_encode + exclusive_scan;
-// CTG_SORTED_RUNS=0 restores the library pair for A/B
+// write) instead of rocPRIM's run_length_encode + exclusive_scan when
+// CTG_SORTED_RUNS=1 (default off until the GPU A/B and parity test of the
+// round have run on hardware)
 static bool sorted_runs_on() {
     const char* e = getenv("CTG_SORTED_RUNS");   // read per call: tests switch it
-    return !(e && e[0] == '0');
+    return e && e[0] == '1';
 }
 static int64_t sort_wide_digits_max() {
     static const int64_t v = [] {

@@ -529,6 +529,7 @@ def test_sorted_runs_match_library_rle(gpu, monkeypatch, packed):
     monkeypatch.setenv('CTG_BUCKET_SORT', '0')
     monkeypatch.setenv('CTG_BUCKET_SORT_PAIRS', '0')
     monkeypatch.setenv('CTG_SORT_PACKED', packed)
+    monkeypatch.setenv('CTG_SORTED_RUNS', '1')
     out = rag.rag_features(lab, bnd)
     monkeypatch.setenv('CTG_SORTED_RUNS', '0')
     ref = rag.rag_features(lab, bnd)
