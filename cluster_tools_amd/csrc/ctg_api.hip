@@ -271,8 +271,9 @@ static bool bucket_sort_pairs_on(int64_t n) {
 }
 // runs of the onesweep-sorted keys by sorted_runs (ctg_sort.hip: count, scan,
 // write) instead of rocPRIM's run_length_encode + exclusive_scan when
-// CTG_SORTED_RUNS=1 (default off until the GPU A/B and parity test of the
-// round have run on hardware)
+// CTG_SORTED_RUNS=1.  Parity-tested, but slower: configs[4] segment 0.98 ->
+// 1.38 ms (4085 chunks of 33 K keys, 132 barrier-separated rounds each), so
+// the library pair stays the default (profiles/r3/s3/ab_sorted_runs.jsonl)
 static bool sorted_runs_on() {
     const char* e = getenv("CTG_SORTED_RUNS");   // read per call: tests switch it
     return e && e[0] == '1';
