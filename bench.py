@@ -7,11 +7,13 @@ resident synthetic volume: face scan (labels uint64 + float32 boundary map in
 HBM) -> per-tile edge records -> radix sort -> per-edge reduction -> sorted
 (E,2) edge table, node list and (E,10) float64 feature table in HBM.
 
-Default (``--config 1``): BASELINE.json configs[1], 512^3 Voronoi supervoxels
-(cell 10, ~1e6 edges) + boundary map per GPU.  N>1 (torch.distributed.run, one
-rank per GPU): weak scaling, each rank owns a 512^3 z-slab of a (512N)x512x512
-volume (+1 halo plane), builds its partial edge table and the ranks combine
-them over RCCL (cluster_tools_amd/dist.py).
+Default (``--config 2``): BASELINE.json configs[2], the north_star volume --
+2048^3 Voronoi supervoxels (cell 16, ~1.6e7 edges) + float32 boundary map,
+103 GB resident on one MI355X at N=1.  N>1 (torch.distributed.run, one rank per
+GPU): strong scaling of the same fixed volume, rank r owns the z-slab
+[2048 r/N, 2048 (r+1)/N) (+1 halo plane below, ``ctg_mgpu_slab``), builds its
+partial edge table and the ranks combine them over RCCL
+(cluster_tools_amd/dist.py).
 
 The other BASELINE configs are extra lines (``--config``), not the driver's
 bench line:
@@ -21,8 +23,8 @@ bench line:
        N5 out; value = end-to-end Gvoxels/s with every job its own process
        (the reference's LocalTask model), plus the same with job threads and
        the compute-only rate of the per-block calls on device-resident inputs
-  2    configs[2]: 2048^3 boundary map (cell 16), strong scaling: the fixed
-       volume is z-sharded over the ranks (2048/N planes each + 1 halo plane)
+  1    configs[1]: 512^3 (cell 10, ~1e6 edges) per GPU; N>1: weak scaling,
+       each rank owns a 512^3 z-slab of a (512N)x512x512 volume
   3    configs[3]: 1024^3, 3-channel nearest-neighbour affinities (N=1)
   3lr  configs[3]: 1024^3, 12-channel long-range affinities (N=1)
   4    configs[4]: 1024^3 high fragmentation (cell 5, ~5e7 edges), strong
@@ -61,12 +63,13 @@ def parse():
     p.add_argument('--gpus', type=int, default=1)
     p.add_argument('--steps', type=int, default=20)
     p.add_argument('--warmup', type=int, default=3)
-    p.add_argument('--config', default='1', choices=sorted(WORKLOADS))
+    p.add_argument('--config', default='2', choices=sorted(WORKLOADS))
     p.add_argument('--size', type=int, default=None, help='cube edge (voxels; per GPU for weak scaling)')
     p.add_argument('--cell', type=int, default=None)
     p.add_argument('--seed', type=int, default=0)
-    p.add_argument('--cpu-baseline-planes', type=int, default=512,
-                   help='z-planes of the per-GPU volume timed with the C oracle (0 = skip)')
+    p.add_argument('--cpu-baseline-planes', type=int, default=None,
+                   help='z-planes of the volume timed with the C oracle (0 = skip; default: 512 of '
+                        'configs[1], 128 of configs[2] = 537 M voxels)')
     p.add_argument('--cpu-threads', type=int, default=min(16, os.cpu_count() or 1),
                    help='worker processes of the CPU baseline (the GPU box allots 16 cores per GPU)')
     p.add_argument('--no-cpu-baseline', action='store_true')
@@ -117,7 +120,10 @@ def cpu_baseline(labels_t, bnd_t, planes, workers):
     lab = labels_t[:planes].cpu().numpy().view(np.uint64)
     bnd = bnd_t[:planes].cpu().numpy()
     workers = max(1, min(workers, planes))
-    tmp = '/dev/shm' if os.path.isdir('/dev/shm') else tempfile.gettempdir()
+    import shutil
+    need = lab.nbytes + bnd.nbytes + (1 << 30)
+    tmp = '/dev/shm' if os.path.isdir('/dev/shm') and shutil.disk_usage('/dev/shm').free > need \
+        else tempfile.gettempdir()
     d = tempfile.mkdtemp(prefix='ctg_cpu_', dir=tmp)
     lp, dp = os.path.join(d, 'labels.npy'), os.path.join(d, 'data.npy')
     try:
@@ -464,8 +470,11 @@ def main():
     line = None
     if rank == 0:
         cpu = None
-        if not args.no_cpu_baseline and args.cpu_baseline_planes > 0 and world == 1 and args.config == '1':
-            v, info = cpu_baseline(lab, bnd, min(args.cpu_baseline_planes, S), args.cpu_threads)
+        planes = args.cpu_baseline_planes
+        if planes is None:
+            planes = {'1': 512, '2': 128}.get(args.config, 0)
+        if not args.no_cpu_baseline and planes > 0 and world == 1 and args.config in ('1', '2'):
+            v, info = cpu_baseline(lab, bnd, min(planes, S), args.cpu_threads)
             cpu = {'value': round(v, 6), 'unit': 'Gvoxels/s', 'cores': info['threads'], 'kind': 'port',
                    'sample': info['sample'] + ', %.2f s slowest worker (best of 2), oracle/ctg_oracle.c scalar C restatement '
                                               '(nifty reference not present on this host)' % info['seconds']}

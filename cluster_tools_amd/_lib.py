@@ -27,6 +27,9 @@ CTG_MAX_CHANNELS = 24
 CTG_N_FEATURES = 10
 CTG_NBINS = 40
 CTG_WIDE_RECORD_WORDS = 48
+CTG_MGPU_SAMPLES = 1024
+CTG_MGPU_ROW_WORDS = 28
+CTG_MGPU_MAX_WORLD = 32
 CTG_IO_N5 = 0
 CTG_IO_ZARR_DOT = 1
 CTG_IO_ZARR_SLASH = 2
@@ -64,6 +67,11 @@ PROTOTYPES = {
     'ctg_merge_stats': (ctypes.c_int, [c_vp, c_vp, c_vp, ctypes.c_int64, ctypes.c_double, ctypes.c_double,
                                        ctypes.c_int, ctypes.c_int, c_vp, ctypes.POINTER(c_vp)]),
     'ctg_mgpu_slab': (ctypes.c_int, [ctypes.c_int64, ctypes.c_int, ctypes.c_int, c_vp, ctypes.c_int, c_vp]),
+    'ctg_mgpu_sample': (ctypes.c_int, [c_vp, c_vp, c_vp]),
+    'ctg_mgpu_split': (ctypes.c_int, [c_vp, c_vp, ctypes.c_int, c_vp, c_vp]),
+    'ctg_mgpu_pack': (ctypes.c_int, [c_vp, c_vp, ctypes.c_int, ctypes.c_int, c_vp, c_vp]),
+    'ctg_mgpu_merge': (ctypes.c_int, [c_vp, c_vp, c_vp, ctypes.c_int, ctypes.c_int, ctypes.c_double,
+                                      ctypes.c_double, c_vp, ctypes.POINTER(c_vp)]),
     'ctg_merge_feature_rows': (ctypes.c_int, [c_vp, c_vp, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, c_vp,
                                               ctypes.c_int, c_vp]),
     'ctg_unique_pairs': (ctypes.c_int, [c_vp, ctypes.c_int64, ctypes.c_int, c_vp, ctypes.POINTER(c_vp)]),

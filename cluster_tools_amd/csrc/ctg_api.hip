@@ -141,6 +141,9 @@ static void dfree(void* p) {
     g_pool[d & 63].emplace(b, p);
 }
 
+void* dev_alloc(size_t bytes) { return dalloc(bytes); }
+void dev_free(void* p) { dfree(p); }
+
 void ensure(void** p, size_t& have, size_t need) {
     if (need <= have && *p) return;
     if (*p) dfree(*p);
@@ -577,6 +580,103 @@ int ctg_mgpu_slab(int64_t Z, int world_size, int rank, const int64_t* offsets, i
     out[0] = z0 - std::min(down, z0);
     out[1] = z0;
     out[2] = z1;
+    return CTG_OK;
+}
+
+static bool mgpu_args(const ctg_result* r, int world, const char* who) {
+    if (!r || world <= 0 || world > CTG_MGPU_MAX_WORLD) {
+        set_error(std::string(who) + ": bad arguments (world size must be 1.." +
+                  std::to_string(CTG_MGPU_MAX_WORLD) + ")");
+        return false;
+    }
+    return true;
+}
+
+int ctg_mgpu_sample(const ctg_result* local, int64_t* meta, void* stream) {
+    DevLock dev_lock;
+    if (!mgpu_args(local, 1, "ctg_mgpu_sample") || !meta) return CTG_ERR_ARG;
+    CTG_CHECK(mgpu_sample(local->edges, local->n_edges, meta, (hipStream_t)stream));
+    return CTG_OK;
+}
+
+int ctg_mgpu_split(const ctg_result* local, const int64_t* meta_all, int world_size, int64_t* counts, void* stream) {
+    DevLock dev_lock;
+    if (!mgpu_args(local, world_size, "ctg_mgpu_split") || !meta_all || !counts) return CTG_ERR_ARG;
+    Workspace& w = ws(cur_dev());
+    CTG_CHECK(ws_init(w));
+    uint64_t* spl = (uint64_t*)dalloc(CTG_MGPU_MAX_WORLD * 8);
+    if (!spl) {
+        set_error("ctg_mgpu_split: out of device memory");
+        return CTG_ERR_NOMEM;
+    }
+    const hipError_t e = mgpu_split(local->edges, local->n_edges, local->nodes, local->n_nodes, meta_all,
+                                    world_size, spl, counts, (hipStream_t)stream);
+    dfree(spl);   // stream-ordered reuse
+    CTG_CHECK(e);
+    return CTG_OK;
+}
+
+int ctg_mgpu_pack(const ctg_result* local, const int64_t* counts_all, int world_size, int rank, int64_t* send,
+                  void* stream) {
+    DevLock dev_lock;
+    if (!mgpu_args(local, world_size, "ctg_mgpu_pack") || !counts_all || rank < 0 || rank >= world_size)
+        return CTG_ERR_ARG;
+    const int64_t* mine = counts_all + (int64_t)rank * world_size * 2;
+    int64_t rows = 0, nodes = 0, words = 0;
+    for (int d = 0; d < world_size; ++d) {
+        rows += mine[2 * d];
+        nodes += mine[2 * d + 1];
+        if (d != rank) words += mine[2 * d] * CTG_MGPU_ROW_WORDS + mine[2 * d + 1];
+    }
+    if (rows != local->n_edges || nodes != local->n_nodes) {
+        set_error("ctg_mgpu_pack: counts do not cover this rank's table");
+        return CTG_ERR_ARG;
+    }
+    if (words > 0 && (!send || !local->stats || !local->stat_sums)) {
+        set_error("ctg_mgpu_pack: rows to send need a CTG_KEEP_STATS table and a send buffer");
+        return CTG_ERR_ARG;
+    }
+    CTG_CHECK(mgpu_pack(local, counts_all, world_size, rank, send, (hipStream_t)stream));
+    return CTG_OK;
+}
+
+int ctg_mgpu_merge(ctg_result* local, const int64_t* recv, const int64_t* counts_all, int world_size, int rank,
+                   double hist_lo, double hist_hi, void* stream, ctg_result** out) {
+    DevLock dev_lock;
+    if (!mgpu_args(local, world_size, "ctg_mgpu_merge") || !counts_all || !out || rank < 0 || rank >= world_size ||
+        !(hist_hi > hist_lo))
+        return CTG_ERR_ARG;
+    *out = nullptr;
+    int64_t rows = 0, nodes = 0, recv_words = 0;
+    for (int d = 0; d < world_size; ++d) {
+        rows += counts_all[((int64_t)rank * world_size + d) * 2];
+        nodes += counts_all[((int64_t)rank * world_size + d) * 2 + 1];
+        if (d != rank)
+            recv_words += counts_all[((int64_t)d * world_size + rank) * 2] * CTG_MGPU_ROW_WORDS +
+                          counts_all[((int64_t)d * world_size + rank) * 2 + 1];
+    }
+    if (rows != local->n_edges || nodes != local->n_nodes) {
+        set_error("ctg_mgpu_merge: counts do not cover this rank's table");
+        return CTG_ERR_ARG;
+    }
+    if (recv_words > 0 && !recv) {
+        set_error("ctg_mgpu_merge: null receive buffer");
+        return CTG_ERR_ARG;
+    }
+    Workspace& w = ws(cur_dev());
+    CTG_CHECK(ws_init(w));
+    ctg_result* r = new ctg_result();
+    r->device = cur_dev();
+    const hipError_t e = mgpu_merge(local, recv, counts_all, world_size, rank, hist_lo, hist_hi,
+                                    (hipStream_t)stream, r);
+    if (e != hipSuccess) {
+        set_error(std::string("ctg_mgpu_merge: ") + hipGetErrorString(e));
+        ctg_free(r);
+        return e == hipErrorOutOfMemory ? CTG_ERR_NOMEM : CTG_ERR_HIP;
+    }
+    local->n_edges = 0;
+    local->n_nodes = 0;
+    *out = r;
     return CTG_OK;
 }
 
@@ -1107,6 +1207,7 @@ int ctg_rag_features(const void* labels, int label_bits, const void* data, int d
         hipEventElapsedTime(&ms, w.ev[0], w.ev[6]);
         w.last_ms[6] = ms;
     }
+    r->partial_adj = J.need_adj == 2 ? 1 : 0;
     *out = r;
     return CTG_OK;
 }
@@ -1408,6 +1509,7 @@ int ctg_rag_blocks(const void* labels, int label_bits, const void* data, int dat
         hipEventElapsedTime(&ms, w.ev[0], w.ev[6]);
         w.last_ms[6] = ms;
     }
+    r->partial_adj = J.need_adj == 2 ? 1 : 0;
     *out = r;
     return CTG_OK;
 }
@@ -1860,9 +1962,13 @@ void ctg_free(ctg_result* r) {
     if (!r) return;
     int d = cur_dev();
     if (r->device >= 0 && r->device != d) hipSetDevice(r->device);
-    dfree(r->edges);
-    dfree(r->nodes);
-    dfree(r->features);
+    if (!r->owned.empty()) {   // the handle's arrays point into these (ctg_mgpu_merge)
+        for (void* p : r->owned) dfree(p);
+    } else {
+        dfree(r->edges);
+        dfree(r->nodes);
+        dfree(r->features);
+    }
     dfree(r->stats);
     dfree(r->stat_sums);
     if (r->device >= 0 && r->device != d) hipSetDevice(d);

@@ -224,6 +224,9 @@ int current_device();
 void set_error(const std::string& msg);
 void ensure(void** p, size_t& have, size_t need);
 hipError_t ensure_records(Workspace& w, int64_t need, int wide);
+// the library's caching device allocator (stream-ordered reuse, ctg_api.hip)
+void* dev_alloc(size_t bytes);
+void dev_free(void* p);
 
 }  // namespace ctg
 
@@ -243,7 +246,24 @@ struct ctg_result {
     double2* stat_sums = nullptr;   // device (E,) (sum, sumsq) or null
     int64_t n_records = 0;
     int64_t n_direct = 0;
+    // affinity partial table (CTG_NO_ADJ_FILTER): a key is an edge only where
+    // some record carries the ADJ bit (decided after a merge)
+    int partial_adj = 0;
+    // allocations this handle frees instead of the five pointers above, which
+    // then point into them (a multi-GPU shard that is a range of its rank's
+    // local table: ctg_mgpu_merge)
+    std::vector<void*> owned;
 };
+
+namespace ctg {
+hipError_t mgpu_sample(const uint64_t* edges, int64_t E, int64_t* meta, hipStream_t s);
+hipError_t mgpu_split(const uint64_t* edges, int64_t E, const uint64_t* nodes, int64_t N, const int64_t* meta_all,
+                      int world, uint64_t* spl, int64_t* counts, hipStream_t s);
+hipError_t mgpu_pack(const ctg_result* r, const int64_t* counts_all, int world, int rank, int64_t* send,
+                     hipStream_t s);
+hipError_t mgpu_merge(ctg_result* local, const int64_t* recv, const int64_t* counts_all, int world, int rank,
+                      double hist_lo, double hist_hi, hipStream_t s, ctg_result* out);
+}  // namespace ctg
 
 #define CTG_CHECK(expr)                                                        \
     do {                                                                       \

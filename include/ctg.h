@@ -167,13 +167,46 @@ int ctg_merge_stats(const uint64_t* keys, const double* sums, const uint32_t* re
  * volume of Z planes and reads [out[0], out[2]): below its owned range as many
  * halo planes as the face / offsets reach down (1 for boundary maps and
  * nearest-neighbour affinities, max(-o_z) for long-range offsets), none for
- * rank 0.  ctg_rag_features' own_begin[0] is out[1] - out[0].  The ranks'
- * partial tables (keep_stats) are combined after the exchange by
- * ctg_merge_stats; the exchange itself runs over RCCL in the host layer
- * (cluster_tools_amd/dist.py).  Positive z offsets (a partner above the slab)
- * with world_size > 1 are CTG_ERR_UNSUPPORTED: the z-slab layout has no upper
- * halo.  Host-only: needs no device. */
+ * rank 0.  ctg_rag_features' own_begin[0] is out[1] - out[0].  Positive z
+ * offsets (a partner above the slab) with world_size > 1 are
+ * CTG_ERR_UNSUPPORTED: the z-slab layout has no upper halo.  Host-only: needs
+ * no device. */
 int ctg_mgpu_slab(int64_t Z, int world_size, int rank, const int64_t* offsets, int n_channels, int64_t* out);
+
+/* Multi-GPU combine of the ranks' partial tables (replaces the
+ * block -> merge step of ndist.mergeSubgraphs, graph/merge_sub_graphs.py:130-135,
+ * and ndist.mergeFeatureBlocks, features/merge_edge_features.py:141-147, at the
+ * scale of whole GPUs).  `local` is a rank's CTG_KEEP_STATS result of its slab
+ * (affinities: also CTG_NO_ADJ_FILTER).  The global sorted edge table is
+ * range-partitioned by u; the host runs the collectives (RCCL over xGMI via
+ * torch.distributed in cluster_tools_amd/dist.py) between these steps, all
+ * arrays in device memory of the current device:
+ *   1. ctg_mgpu_sample -> meta (CTG_MGPU_SAMPLES + 1 int64): evenly spaced u
+ *      values (unsigned order as int64: u xor 2^63) and the edge count;
+ *      all_gather of meta -> meta_all (world x (CTG_MGPU_SAMPLES + 1));
+ *   2. ctg_mgpu_split -> counts (world x 2 int64): rows and node ids this rank
+ *      sends to each rank (its own entry: what it keeps); all_gather ->
+ *      counts_all (world x world x 2, [src][dst][rows, nodes]), read to host;
+ *   3. ctg_mgpu_pack -> send (int64 words): for every dst != rank with data, in
+ *      rank order, rows x CTG_MGPU_ROW_WORDS words ((u, v), (S1, S2) bits, the
+ *      48-word wide record) then the node ids; all_to_all with those sizes ->
+ *      recv (segments of every src != rank in rank order);
+ *   4. ctg_mgpu_merge -> *out: this rank's shard of the global table (sorted
+ *      edges, features, nodes); equal keys combine exactly (counts and
+ *      histograms add, moments by Chan's rule), affinity partials keep keys
+ *      whose ADJ bit some record carries.  `local`'s arrays move into the shard
+ *      (a range of them when nothing was received: no copy); ctg_free(local)
+ *      is still required.  counts_all is host memory.
+ * world_size <= CTG_MGPU_MAX_WORLD. */
+#define CTG_MGPU_SAMPLES 1024
+#define CTG_MGPU_ROW_WORDS 28
+#define CTG_MGPU_MAX_WORLD 32
+int ctg_mgpu_sample(const ctg_result* local, int64_t* meta, void* stream);
+int ctg_mgpu_split(const ctg_result* local, const int64_t* meta_all, int world_size, int64_t* counts, void* stream);
+int ctg_mgpu_pack(const ctg_result* local, const int64_t* counts_all, int world_size, int rank, int64_t* send,
+                  void* stream);
+int ctg_mgpu_merge(ctg_result* local, const int64_t* recv, const int64_t* counts_all, int world_size, int rank,
+                   double hist_lo, double hist_hi, void* stream, ctg_result** out);
 
 /* Merge reference-layout feature rows (n x 10 float64, [mean, var, min,
  * q10..q90, max, count]) of global edges ids[i] in [id_begin, id_end) into

@@ -61,35 +61,174 @@ def decode_stats(sums, rec):
                 hist=rec[:, :O.NBINS + 2].astype(np.int64))
 
 
+SIGN = np.uint64(1 << 63)
+S = 1024          # CTG_MGPU_SAMPLES
+ROW = 28          # CTG_MGPU_ROW_WORDS
+
+
+class Part:
+    """A rank's partial table (the numpy twin of a CTG_KEEP_STATS result)."""
+
+    def __init__(self, edges, feats, sums, rec, nodes, partial_adj):
+        self.edges, self.feats, self.sums, self.rec, self.nodes = edges, feats, sums, rec, nodes
+        self.partial_adj = partial_adj
+
+    def info(self):
+        return (0, 0)
+
+    def free(self):
+        pass
+
+
+class NumpyShard:
+    """The rag.Result accessors the distributed code and the tests use."""
+
+    def __init__(self, edges, feats, nodes):
+        self._e = np.ascontiguousarray(edges, dtype=np.uint64).reshape(-1, 2)
+        self._f = np.ascontiguousarray(feats, dtype=np.float64).reshape(-1, O.N_FEATURES)
+        self._n = np.ascontiguousarray(nodes, dtype=np.uint64).reshape(-1)
+
+    n_edges = property(lambda self: self._e.shape[0])
+    n_nodes = property(lambda self: self._n.shape[0])
+
+    def edges(self):
+        return self._e
+
+    def features(self):
+        return self._f
+
+    def nodes(self):
+        return self._n
+
+    def edges_torch_i64(self):
+        return torch.from_numpy(self._e.view(np.int64))
+
+    def features_torch(self):
+        return torch.from_numpy(self._f)
+
+    def nodes_torch(self):
+        return torch.from_numpy(self._n.view(np.int64))
+
+    def free(self):
+        pass
+
+
+def splitters(meta_all, world):
+    """Restatement of k_mgpu_splitters (ctg_mgpu.hip): sample j of rank r
+    (value v) has the integer cumulative weight CW = sum_q count_q * c_q (c_q:
+    samples of rank q at or before it in the (v, r, j) order); splitter k is
+    the v whose interval (CW - count_r, CW] holds total * S * k / world."""
+    m = np.asarray(meta_all, dtype=np.int64).reshape(world, S + 1)
+    cnt = m[:, S].astype(np.uint64)
+    total = int(cnt.sum())
+    spl = np.zeros(max(world - 1, 0), dtype=np.uint64)
+    for r in range(world):
+        if cnt[r] == 0:
+            continue
+        v = m[r, :S]
+        cw = np.zeros(S, dtype=object)
+        for q in range(world):
+            if cnt[q] == 0:
+                continue
+            row = m[q, :S]
+            c = (np.searchsorted(row, v, side='right') if q < r else
+                 np.searchsorted(row, v, side='left') if q > r else np.arange(1, S + 1))
+            cw = cw + int(cnt[q]) * c.astype(object)
+        for k in range(1, world):
+            t = total * S * k
+            hit = [(int(a) - int(cnt[r])) * world < t <= int(a) * world for a in cw]
+            for j in np.nonzero(hit)[0]:
+                spl[k - 1] = np.uint64(v[j]) ^ SIGN
+    return spl
+
+
+def split_counts(part, spl, world):
+    """Restatement of k_mgpu_bounds: rows / node ids per rank's u range."""
+    u = part.edges[:, 0] if part.edges.shape[0] else np.zeros(0, np.uint64)
+    eb = [0] + [int(np.searchsorted(u, x, side='left')) for x in spl] + [u.shape[0]]
+    nb = [0] + [int(np.searchsorted(part.nodes, x, side='left')) for x in spl] + [part.nodes.shape[0]]
+    return np.array([[max(eb[d + 1] - eb[d], 0), max(nb[d + 1] - nb[d], 0)] for d in range(world)], np.int64)
+
+
 class OracleBackend:
+    """The four device steps of dist.py's exchange restated in numpy over the
+    oracle's statistics (ctg_mgpu_sample / split / pack / merge)."""
+
     def local(self, labels, data, offsets, own_begin, own_end, ignore_label, hist_range):
         lab = np.asarray(labels)
         edges, feats, stats = O.boundary_features(lab, np.asarray(data), own_begin=own_begin,
                                                   ignore_label=ignore_label, lo=hist_range[0], hi=hist_range[1],
                                                   return_stats=True)
         sums, rec = encode_stats(stats)
-        nodes = np.unique(edges.reshape(-1))
-        return (torch.from_numpy(edges.astype(np.int64)), torch.from_numpy(sums),
-                torch.from_numpy(rec.view(np.int32)), torch.from_numpy(nodes.astype(np.int64)), (0, 0),
-                torch.from_numpy(np.ascontiguousarray(feats)))
+        nodes = np.unique(edges.reshape(-1)).astype(np.uint64)
+        return Part(edges.astype(np.uint64).reshape(-1, 2), np.ascontiguousarray(feats), sums, rec, nodes, False)
 
-    def merge(self, keys, sums, recs, hist_range):
-        k = keys.numpy().astype(np.uint64)
-        if k.shape[0] == 0:
-            return torch.zeros((0, 2), dtype=torch.int64), torch.zeros((0, O.N_FEATURES), dtype=torch.float64)
-        edges, inv = O._unique_pairs(k, return_inverse=True)
-        rec = recs.numpy().view(np.uint32)
-        st = decode_stats(sums.numpy(), rec)
+    def sample(self, part):
+        E = part.edges.shape[0]
+        meta = np.zeros(S + 1, dtype=np.int64)
+        if E:
+            idx = (np.arange(S, dtype=np.int64) * E) // S
+            meta[:S] = (part.edges[idx, 0] ^ SIGN).view(np.int64)
+        meta[S] = E
+        return torch.from_numpy(meta)
+
+    def split(self, part, meta_all, world):
+        return torch.from_numpy(split_counts(part, splitters(meta_all.numpy(), world), world))
+
+    def pack(self, part, counts_all, world, rank, words):
+        c = np.asarray(counts_all).reshape(world, world, 2)[rank]
+        e0 = np.concatenate([[0], np.cumsum(c[:, 0])])
+        n0 = np.concatenate([[0], np.cumsum(c[:, 1])])
+        out = []
+        for d in range(world):
+            if d == rank:
+                continue
+            a, b = e0[d], e0[d + 1]
+            rows = np.concatenate([part.edges[a:b].view(np.int64), part.sums[a:b].view(np.int64),
+                                   np.ascontiguousarray(part.rec[a:b]).view(np.int64)], axis=1)
+            out.append(rows.reshape(-1))
+            out.append(part.nodes[n0[d]:n0[d + 1]].view(np.int64))
+        w = np.concatenate(out) if out else np.zeros(0, np.int64)
+        assert w.shape[0] == words
+        return torch.from_numpy(w)
+
+    def merge(self, part, recv, counts_all, world, rank, hist_range):
+        c = np.asarray(counts_all).reshape(world, world, 2)
+        e_lo, n_lo = int(c[rank, :rank, 0].sum()), int(c[rank, :rank, 1].sum())
+        e_cnt, n_cnt = int(c[rank, rank, 0]), int(c[rank, rank, 1])
+        own_e, own_f = part.edges[e_lo:e_lo + e_cnt], part.feats[e_lo:e_lo + e_cnt]
+        own_s, own_r = part.sums[e_lo:e_lo + e_cnt], part.rec[e_lo:e_lo + e_cnt]
+        rk, rs, rr, rn = [], [], [], []
+        w = recv.numpy() if recv is not None else np.zeros(0, np.int64)
+        off = 0
+        for q in range(world):
+            if q == rank:
+                continue
+            nr, nn = int(c[q, rank, 0]), int(c[q, rank, 1])
+            rows = w[off:off + nr * ROW].reshape(nr, ROW)
+            rk.append(rows[:, :2].view(np.uint64))
+            rs.append(rows[:, 2:4].copy().view(np.float64))
+            rr.append(np.ascontiguousarray(rows[:, 4:]).view(np.uint32).reshape(nr, WIDE))
+            rn.append(w[off + nr * ROW:off + nr * ROW + nn].view(np.uint64))
+            off += nr * ROW + nn
+        nodes = part.nodes[n_lo:n_lo + n_cnt]
+        if rn and sum(x.shape[0] for x in rn):
+            nodes = np.unique(np.concatenate([nodes] + rn))
+        M = sum(x.shape[0] for x in rk)
+        if M == 0 and not part.partial_adj:
+            return NumpyShard(own_e, own_f, nodes)
+        keys = np.concatenate([own_e] + rk)
+        sums = np.concatenate([own_s] + rs)
+        rec = np.concatenate([own_r] + rr)
+        edges, inv = O._unique_pairs(keys, return_inverse=True)
+        st = decode_stats(sums, rec)
         merged = O.merge_feature_stats([(inv, st)], edges.shape[0], hist_range[0], hist_range[1])
         feats = O.finalize_features(merged, hist_range[0], hist_range[1])
-        # ctg_merge_stats keeps only keys with the ADJ bit on some row (need_adj):
-        # the exchange's empty slots (keys (j, j), zero records) disappear here
+        touched = np.zeros(edges.shape[0], bool)
+        touched[inv[e_cnt:]] = True
+        keep_own = ~touched[inv[:e_cnt]]
+        feats[inv[:e_cnt][keep_own]] = own_f[keep_own]     # untouched own rows: the local call's features
         adj = np.zeros(edges.shape[0], bool)
         np.logical_or.at(adj, inv, (rec[:, 42] & ADJ) != 0)
-        return (torch.from_numpy(edges[adj].astype(np.int64)),
-                torch.from_numpy(np.ascontiguousarray(feats[adj])))
-
-    def unique(self, values):
-        """sorted unique ids in unsigned order (as ctg_unique_labels)"""
-        u = np.unique(values.numpy().view(np.uint64))
-        return torch.from_numpy(u.view(np.int64))
+        keep = adj if part.partial_adj else np.ones(edges.shape[0], bool)
+        return NumpyShard(edges[keep], feats[keep], nodes)

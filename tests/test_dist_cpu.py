@@ -1,4 +1,4 @@
-"""Multi-rank logic of cluster_tools_amd/dist.py on CPU (gloo, world_size 2 and 3).
+"""Multi-rank logic of cluster_tools_amd/dist.py on CPU (gloo, world sizes 1-8).
 
 Each rank holds one z-slab (+ the halo plane below it) of a synthetic volume,
 builds its partial table with the oracle-backed backend, and the real
@@ -103,44 +103,84 @@ def test_distributed_matches_whole_volume(tmp_path, world, shape, cell, ignore, 
         assert all(len(x) > 0 for x in es)
 
 
-def test_weighted_splitters_balance():
+def _meta(keys_per_rank):
+    """meta rows (CTG_MGPU_SAMPLES evenly spaced u of sorted keys, + count) as ctg_mgpu_sample writes them."""
+    from tests.dist_helpers import S
+    rows = []
+    for k in keys_per_rank:
+        k = np.sort(np.asarray(k, dtype=np.uint64))
+        m = np.zeros(S + 1, np.int64)
+        if k.size:
+            m[:S] = (k[(np.arange(S) * k.size) // S] ^ np.uint64(1 << 63)).view(np.int64)
+        m[S] = k.size
+        rows.append(m)
+    return np.stack(rows)
+
+
+def test_splitters_balance_and_agree():
+    """The integer-weight splitter rule (restated from k_mgpu_splitters)
+    balances skewed ranks and is a pure function of the gathered samples."""
+    from tests.dist_helpers import splitters
     rng = np.random.default_rng(0)
-    keys = [np.sort(rng.integers(r * 1000, r * 1000 + 1500, size=n)) for r, n in enumerate([5000, 100, 9000])]
-    S = 64
-    samples = np.stack([k[(np.arange(S) * len(k)) // S] for k in keys])
-    sp = cdist.weighted_splitters(samples, [len(k) for k in keys], 3)
+    keys = [rng.integers(r * 1000, r * 1000 + 1500, size=n).astype(np.uint64) for r, n in enumerate([5000, 100, 9000])]
+    sp = splitters(_meta(keys), 3)
     assert sp.shape == (2,) and sp[0] <= sp[1]
     allk = np.sort(np.concatenate(keys))
     owner = np.searchsorted(sp, allk, side='right')
     frac = np.bincount(owner, minlength=3) / allk.size
     assert np.all(np.abs(frac - 1 / 3) < 0.05)
+    np.testing.assert_array_equal(sp, splitters(_meta(keys), 3))
 
 
-def test_weighted_splitters_empty_ranks():
-    sp = cdist.weighted_splitters(np.zeros((4, 8), np.int64), [0, 0, 0, 0], 4)
-    assert sp.shape == (3,)
-    sp = cdist.weighted_splitters(np.array([[5] * 8, [0] * 8]), [10, 0], 2)
+def test_splitters_empty_ranks():
+    from tests.dist_helpers import splitters
+    assert list(splitters(_meta([[], [], [], []]), 4)) == [0, 0, 0]
+    sp = splitters(_meta([[5] * 10, []]), 2)
     assert list(sp) == [5]
+    # labels >= 2^63: unsigned order survives the int64 samples
+    big = np.uint64(1 << 63)
+    sp = splitters(_meta([np.arange(100, dtype=np.uint64) + big, np.arange(100, dtype=np.uint64)]), 2)
+    assert sp[0] < big
 
 
-def test_split_counts_and_rows_roundtrip():
-    k = torch.tensor([1, 1, 2, 5, 5, 5, 9], dtype=torch.int64)
-    assert cdist.split_counts(k, np.array([2, 6])) == [2, 4, 1]
-    assert cdist.split_counts(k, np.array([0, 100])) == [0, 7, 0]
-    assert cdist.split_counts(k, np.array([], np.int64)) == [7]
-    n = 5
-    keys = torch.arange(2 * n, dtype=torch.int64).reshape(n, 2)
-    sums = torch.rand(n, 2, dtype=torch.float64)
-    recs = torch.randint(-2 ** 31, 2 ** 31 - 1, (n, 48), dtype=torch.int32)
-    rows = cdist.pack_rows(keys, sums, recs)
-    assert rows.shape == (n, cdist.ROW_WORDS)
-    k2, s2, r2 = cdist.unpack_rows(rows)
-    assert torch.equal(k2, keys) and torch.equal(s2, sums) and torch.equal(r2, recs)
+def test_segment_words():
+    c = np.zeros((3, 3, 2), np.int64)
+    c[0, 1] = (2, 5)
+    c[2, 1] = (1, 0)
+    c[1, 1] = (7, 7)
+    send, recv = cdist.segment_words(c, 3, 1)
+    assert send == [0, 0, 0] and recv == [2 * cdist.ROW_WORDS + 5, 0, cdist.ROW_WORDS]
+    assert cdist._any_exchange(c, 3)
+    diag = np.zeros((3, 3, 2), np.int64)
+    for r in range(3):
+        diag[r, r] = (4, 4)
+    assert not cdist._any_exchange(diag, 3)
+
+
+def test_exchange_in_one_process_matches_whole_volume():
+    """The four exchange steps of every rank simulated in one process (the
+    collectives replaced by stacking / slicing; tests/exchange_sim.py): the
+    shards concatenate to the whole-volume oracle."""
+    from tests.dist_helpers import OracleBackend
+    from tests.exchange_sim import simulate
+    shape = (30, 26, 24)
+    lab, bnd = _volume(shape, 5, False)
+    e_ref, f_ref = O.boundary_features(lab, bnd)
+    n_ref = O.unique_labels(O.rag_edges(lab))
+    for world in (1, 2, 3, 5):
+        shards = simulate(OracleBackend(), lab, bnd, world)
+        e = np.concatenate([s.edges() for s in shards])
+        f = np.concatenate([s.features() for s in shards])
+        n = np.concatenate([s.nodes() for s in shards])
+        np.testing.assert_array_equal(e, e_ref)
+        np.testing.assert_allclose(f, f_ref, rtol=1e-9, atol=1e-12)
+        np.testing.assert_array_equal(n, n_ref)
 
 
 def test_slab_halo_checked_against_offsets():
     """dist.py refuses affinity offsets that reach past the slab's halo
-    instead of silently dropping the samples whose partner lies below it."""
+    instead of silently dropping the samples whose partner lies below it --
+    unless the slab plan clipped the halo at plane 0 (tiny slabs)."""
     lr = synthetic.LR_OFFSETS
     cdist.check_slab_halo((40, 8, 8), lr, (27, 0, 0), None)        # enough halo planes
     cdist.check_slab_halo((40, 8, 8), lr, (0, 0, 0), None)         # bottom slab: no neighbour below
@@ -150,70 +190,51 @@ def test_slab_halo_checked_against_offsets():
         cdist.check_slab_halo((40, 8, 8), lr, (1, 0, 0), None)
     with pytest.raises(ValueError, match='upper halo'):
         cdist.check_slab_halo((40, 8, 8), [[2, 0, 0]], (1, 0, 0), None)
+    # 16 planes over 8 ranks, offset -4: rank 1 owns [2, 4) and reads from plane 0
+    for r in range(8):
+        rd, own, end = cdist.slab_plan(16, 8, r, [[-4, 0, 0]])
+        cdist.check_slab_halo((end - rd, 8, 8), [[-4, 0, 0]], (own - rd, 0, 0), None, read_begin=rd)
 
 
-def test_device_splitters_match_numpy_restatement():
-    rng = np.random.default_rng(5)
-    for world in (2, 4, 8):
-        counts = rng.integers(0, 5000, world)
-        counts[rng.integers(0, world)] = 0
-        S = 32
-        samples = np.sort(rng.integers(-2 ** 62, 2 ** 62, (world, S)), axis=1)
-        sp = cdist.weighted_splitters(samples, counts, world)
-        # restatement: weighted quantiles of the kept samples
-        w = np.repeat(counts / S, S)
-        v = samples.reshape(-1)
-        v, w = v[w > 0], w[w > 0]
-        o = np.argsort(v, kind='stable')
-        v, w = v[o], w[o]
-        cw = np.cumsum(w)
-        idx = np.minimum(np.searchsorted(cw, cw[-1] * np.arange(1, world) / world, side='left'), v.size - 1)
-        np.testing.assert_array_equal(sp, v[idx])
-
-
-def _plan_worker(rank, world, port, outdir):
-    """Four calls on the same slab: the first learns the ExchangePlan, the
-    second reuses it (no host read before the result-size read), the third
-    starts from exchange capacities too small for its counts (overflow ->
-    regrow -> redo), the fourth from a too small merge slice (redone locally)."""
+def _reads_worker(rank, world, port, outdir):
+    """Two calls with different slab shapes (Z = 100, then 101 over W = 3: the
+    slabs differ between the ranks and between the calls); the host reads of
+    every call are recorded."""
     import torch.distributed as dist
     from tests.dist_helpers import OracleBackend
     os.environ['MASTER_ADDR'] = '127.0.0.1'
     os.environ['MASTER_PORT'] = str(port)
     dist.init_process_group('gloo', rank=rank, world_size=world)
-    shape = (8 * world, 30, 28)
-    lab, bnd = _volume(shape, 5, False)
-    z0 = [shape[0] * r // world for r in range(world + 1)]
-    halo = 1 if rank > 0 else 0
-    sl = slice(z0[rank] - halo, z0[rank + 1])
-    args = (np.ascontiguousarray(lab[sl]), np.ascontiguousarray(bnd[sl]))
-    outs, reads = [], []
-    for call, plan in enumerate([None, None, cdist.ExchangePlan(1, 1), cdist.ExchangePlan(1 << 16, 1 << 16, 1)]):
+    reads = []
+    for Z in (100, 101):
+        lab, bnd = _volume((Z, 14, 12), 4, False)
+        rd, own, end = cdist.slab_plan(Z, world, rank)
         del cdist.host_reads[:]
-        res = cdist.rag_features_distributed(*args, own_begin=(halo, 0, 0), backend=OracleBackend(), plan=plan)
-        reads.append(list(cdist.host_reads))
-        outs.append((np.asarray(res.edges()), np.asarray(res.features()), res.node_shard.numpy()))
-    for a in outs[1:]:
-        for x, y in zip(a, outs[0]):
-            np.testing.assert_array_equal(x, y)
-    np.save(os.path.join(outdir, 'reads%d.npy' % rank), np.array(['|'.join(r) for r in reads]))
+        res = cdist.rag_features_distributed(np.ascontiguousarray(lab[rd:end]), np.ascontiguousarray(bnd[rd:end]),
+                                             own_begin=(own - rd, 0, 0), backend=OracleBackend())
+        reads.append('|'.join(cdist.host_reads))
+        np.save(os.path.join(outdir, 'e%d_%d.npy' % (Z, rank)), res.edges())
+        np.save(os.path.join(outdir, 'f%d_%d.npy' % (Z, rank)), res.features())
+    np.save(os.path.join(outdir, 'reads%d.npy' % rank), np.array(reads))
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize('world', [2, 4])
-def test_exchange_plan_reuse_and_overflow(tmp_path, world):
-    mp.spawn(_plan_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+def test_changing_slab_shapes_and_host_reads(tmp_path):
+    """No state is carried between calls (a capacity plan cached
+    per slab shape could disagree between ranks): Z = 100 then Z = 101 over 3
+    ranks both equal the whole-volume oracle, and every call reads exactly the
+    count matrix and the shard sizes on the host."""
+    world = 3
+    mp.spawn(_reads_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    for Z in (100, 101):
+        lab, bnd = _volume((Z, 14, 12), 4, False)
+        e_ref, f_ref = O.boundary_features(lab, bnd)
+        e = np.concatenate([np.load(tmp_path / ('e%d_%d.npy' % (Z, r))) for r in range(world)])
+        f = np.concatenate([np.load(tmp_path / ('f%d_%d.npy' % (Z, r))) for r in range(world)])
+        np.testing.assert_array_equal(e, e_ref)
+        np.testing.assert_allclose(f, f_ref, rtol=1e-9, atol=1e-12)
     for r in range(world):
-        reads = list(np.load(tmp_path / ('reads%d.npy' % r)))
-        # (the shard offsets are read after the result size)
-        assert reads[0] == 'plan|plan|result|offsets'      # first call of the shape: learns its capacities
-        assert reads[1] == 'result|offsets'                # plan reused: nothing read before the result size
-        # exchange capacity too small: overflow seen with the result, exchange redone
-        # (the merge slice sized on the truncated exchange may need a local redo too)
-        assert reads[2].startswith('plan|result|result') and reads[2].endswith('|offsets')
-        assert 'plan' not in reads[2][5:]
-        # merge-slice capacity too small: this rank redoes its merge alone (no collective)
-        assert reads[3].startswith('result|') and reads[3].endswith('|offsets')
+        assert list(np.load(tmp_path / ('reads%d.npy' % r))) == ['counts|offsets'] * 2
 
 
 def test_mgpu_slab_plan_c_abi():

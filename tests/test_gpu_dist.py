@@ -88,7 +88,7 @@ def _rccl_worker(rank, world, port, outdir, affinity):
     offs = synthetic.NN_OFFSETS if affinity else None
     lab, bnd = rag.synth_volume(SHAPE, cell=7, seed=9)
     data = rag.synth_affinities(bnd, offs) if affinity else bnd
-    for _ in range(2):   # the second call reuses the learned ExchangePlan
+    for _ in range(2):   # two calls: no state is carried between them
         del cdist.host_reads[:]
         res = cdist.rag_features_distributed(lab, data, offsets=offs, own_begin=(0, 0, 0))
     np.save(os.path.join(outdir, 'e.npy'), res.edges())
@@ -111,5 +111,47 @@ def test_rccl_world1_exchange_equals_single_call(tmp_path, affinity):
     np.testing.assert_array_equal(np.load(tmp_path / 'e.npy'), ref['edges'])
     np.testing.assert_allclose(np.load(tmp_path / 'f.npy'), ref['features'], rtol=1e-9, atol=1e-12)
     np.testing.assert_array_equal(np.load(tmp_path / 'n.npy').astype(np.uint64), ref['nodes'])
-    # plan reused: no host read before the result size
-    assert list(np.load(tmp_path / 'reads.npy')) == ['result', 'offsets']
+    # one count-matrix read and one shard-size read per call
+    assert list(np.load(tmp_path / 'reads.npy')) == ['counts', 'offsets']
+
+
+@pytest.mark.parametrize('affinity', [False, True])
+def test_mgpu_exchange_simulated_in_one_process(affinity):
+    """ctg_mgpu_sample / split / pack / merge of every rank in one process
+    (tests/exchange_sim.py: the collectives replaced by their data movement)
+    at world sizes 1-5: the shards concatenate to the single-call result --
+    edges and nodes bit-exact, features within 1e-9 -- and the HIP split
+    equals the numpy restatement of the splitter rule on the same samples."""
+    from cluster_tools_amd import dist as cdist
+    from cluster_tools_amd import rag
+    from cluster_tools_amd import synthetic
+    from tests.dist_helpers import splitters, split_counts, Part
+    from tests.exchange_sim import simulate
+    offs = synthetic.NN_OFFSETS if affinity else None
+    lab, bnd = rag.synth_volume(SHAPE, cell=7, seed=9)
+    data = rag.synth_affinities(bnd, offs) if affinity else bnd
+    ref = rag.rag_features(lab.cpu().numpy().view(np.uint64), data.cpu().numpy(), offsets=offs)
+    backend = cdist.HipBackend()
+    for world in (1, 2, 3, 5):
+        shards = simulate(backend, lab, data, world, offsets=offs)
+        e = np.concatenate([x.edges() for x in shards])
+        f = np.concatenate([x.features() for x in shards])
+        n = np.concatenate([x.nodes() for x in shards])
+        np.testing.assert_array_equal(e, ref['edges'])
+        np.testing.assert_allclose(f, ref['features'], rtol=1e-9, atol=1e-12)
+        np.testing.assert_array_equal(n, ref['nodes'])
+        for x in shards:
+            x.free()
+    # the split kernel against its restatement: a world-3 sample of this table
+    loc = backend.local(lab, data, offs, (0, 0, 0), None, False, (0.0, 1.0))
+    rng = np.random.default_rng(1)
+    meta = backend.sample(loc).cpu().numpy()
+    metas = [meta]
+    for _ in range(2):
+        m = np.sort(rng.choice(meta[:-1], size=meta.shape[0] - 1))
+        metas.append(np.concatenate([m, [int(rng.integers(1, 10 ** 6))]]))
+    meta_all = np.stack(metas).astype(np.int64)
+    got = backend.split(loc, torch.from_numpy(meta_all).cuda(), 3).cpu().numpy()
+    part = Part(loc.edges(), None, None, None, loc.nodes(), False)
+    np.testing.assert_array_equal(got, split_counts(part, splitters(meta_all, 3), 3))
+    loc.free()
