@@ -108,13 +108,14 @@ def _wire_device(device, group):
     return torch.device('cpu') if dist.get_backend(group) == 'gloo' else device
 
 
-def all_gather_tensor(t, group=None):
-    """all_gather of equal-shape tensors -> list (on t's device)."""
+def all_gather_flat(t, group=None):
+    """all_gather of equal-size tensors into one flat tensor (rank-major, on
+    t's device): one ``all_gather_into_tensor``, no per-rank outputs."""
     wire = _wire_device(t.device, group)
-    tw = t.to(wire)
-    out = [torch.empty_like(tw) for _ in range(dist.get_world_size(group))]
-    dist.all_gather(out, tw, group=group)
-    return [x.to(t.device) for x in out]
+    tw = t.reshape(-1).to(wire)
+    out = torch.empty(tw.numel() * dist.get_world_size(group), dtype=tw.dtype, device=wire)
+    dist.all_gather_into_tensor(out, tw, group=group)
+    return out.to(t.device)
 
 
 # Every device -> host read of the exchange goes through _host(): the tests
@@ -183,8 +184,8 @@ class DistResult:
 def _exclusive_offsets(n_locals, group, device):
     """[(offset of this rank, total)] for each local count, one all_gather;
     and every rank's counts."""
-    t = torch.tensor(list(n_locals), dtype=torch.int64, device=device)
-    allc = _host(torch.stack(all_gather_tensor(t, group)), 'offsets').tolist()
+    t = torch.tensor(list(n_locals), dtype=torch.int64, device=_wire_device(device, group))
+    allc = _host(all_gather_flat(t, group), 'offsets').reshape(-1, len(n_locals)).tolist()
     r = dist.get_rank(group)
     return ([(sum(row[k] for row in allc[:r]), sum(row[k] for row in allc)) for k in range(len(n_locals))],
             [tuple(row) for row in allc])
@@ -263,9 +264,9 @@ def rag_features_distributed(labels, data=None, offsets=None, own_begin=None, ow
         meta = backend.sample(loc)
         dev = meta.device
         wire = _wire_device(dev, group)
-        meta_all = torch.stack(all_gather_tensor(meta, group))
+        meta_all = all_gather_flat(meta, group)
         counts = backend.split(loc, meta_all, world)
-        counts_all = _host(torch.stack(all_gather_tensor(counts, group)), 'counts').numpy()
+        counts_all = _host(all_gather_flat(counts, group), 'counts').numpy().reshape(world, world, 2)
         phase('splitters+counts')
         send_w, recv_w = segment_words(counts_all, world, rank)
         recv = None

@@ -381,46 +381,35 @@ def test_unique_and_map_helpers(gpu):
 
 
 def test_hip_backend_slabs_merge(gpu):
-    """The multi-GPU data path (local partials -> packed rows -> merge) on one
-    GPU: two slabs processed by HipBackend, rows packed/unpacked as dist.py
-    ships them, merged on the device == whole volume."""
-    import torch
+    """The multi-GPU data path (local partials -> ctg_mgpu_split / pack ->
+    exchanged rows -> ctg_mgpu_merge) for 2 and 3 z-slabs on one GPU
+    (tests/exchange_sim.py) == the oracle's whole-volume features."""
     from cluster_tools_amd import dist as cdist
+    from tests.exchange_sim import simulate
     shape = (40, 48, 56)
     lab, bnd = rag.synth_volume(shape, cell=6, seed=21)
-    be = cdist.HipBackend()
-    parts = []
-    for z0, z1 in ((0, 17), (17, 40)):
-        h = 1 if z0 else 0
-        k, s, r, n, _, _f = be.local(lab[z0 - h:z1].contiguous(), bnd[z0 - h:z1].contiguous(), None,
-                                 (h, 0, 0), None, False, (0.0, 1.0))
-        parts.append(cdist.pack_rows(k, s, r))
-    k, s, r = cdist.unpack_rows(torch.cat(parts))
-    me, mf = be.merge(k, s, r, (0.0, 1.0))
     e_ref, f_ref = O.boundary_features(lab.cpu().numpy().view(np.uint64), bnd.cpu().numpy())
-    np.testing.assert_array_equal(me.cpu().numpy().view(np.uint64), e_ref)
-    check_features(mf.cpu().numpy(), f_ref)
+    for world in (2, 3):
+        shards = simulate(cdist.HipBackend(), lab, bnd, world)
+        np.testing.assert_array_equal(np.concatenate([x.edges() for x in shards]), e_ref)
+        check_features(np.concatenate([x.features() for x in shards]), f_ref)
 
 
 def test_hip_backend_affinity_slabs_merge(gpu):
-    import torch
+    """The same with long-range affinities (halo = max(-o_z) planes from the
+    slab plan): per-slab partials keep non-adjacent pairs, the merge keeps the
+    keys whose ADJ bit some slab proved."""
     from cluster_tools_amd import dist as cdist
+    from tests.exchange_sim import simulate
     shape = (30, 40, 40)
     lab, bnd = rag.synth_volume(shape, cell=5, seed=22)
     offs = [[-1, 0, 0], [0, -1, 0], [0, 0, -1], [-2, 0, 0], [0, -3, 0], [0, 0, -3]]
     affs = rag.synth_affinities(bnd, offs)
-    be = cdist.HipBackend()
-    parts = []
-    for z0, z1 in ((0, 13), (13, 30)):
-        h = 2 if z0 else 0                                # halo = max |z offset|
-        k, s, r, n, _, _f = be.local(lab[z0 - h:z1].contiguous(), affs[:, z0 - h:z1].contiguous(), offs,
-                                 (h, 0, 0), None, False, (0.0, 1.0))
-        parts.append(cdist.pack_rows(k, s, r))
-    k, s, r = cdist.unpack_rows(torch.cat(parts))
-    me, mf = be.merge(k, s, r, (0.0, 1.0))
     e_ref, f_ref = O.affinity_features(lab.cpu().numpy().view(np.uint64), affs.cpu().numpy(), offs)
-    np.testing.assert_array_equal(me.cpu().numpy().view(np.uint64), e_ref)
-    check_features(mf.cpu().numpy(), f_ref)
+    for world in (2, 3):
+        shards = simulate(cdist.HipBackend(), lab, affs, world, offsets=offs)
+        np.testing.assert_array_equal(np.concatenate([x.edges() for x in shards]), e_ref)
+        check_features(np.concatenate([x.features() for x in shards]), f_ref)
 
 
 # ------------------------------------------------------- labels >= 2^32
