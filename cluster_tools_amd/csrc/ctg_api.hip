@@ -18,7 +18,6 @@
 namespace ctg {
 hipError_t launch_face_scan(const ScanParams& P, const RecordBuf& R, Counters* C, hipStream_t s);
 int scan_tile_rows();
-hipError_t launch_narrow_labels(const uint64_t* L, uint32_t* out, int64_t n, uint32_t* ovf, hipStream_t s);
 hipError_t launch_density(const void* L, int label_bits, const int64_t* shape, int n_rows, uint32_t* out,
                           hipStream_t s);
 hipError_t launch_unique_tiles(const uint64_t* L, const int64_t* shape, const int64_t* b, const int64_t* e,
@@ -31,8 +30,6 @@ hipError_t bucket_sort_keys(const uint64_t* keys, uint64_t* tmp, uint64_t* out, 
                             uint32_t* small, void** temp, size_t* temp_bytes, hipStream_t s);
 hipError_t bucket_runs(const uint64_t* sorted, int64_t n, int lo_bit, int hi_bit, uint32_t* small, uint64_t* uniq,
                        uint32_t* runs, uint32_t* roffs, uint32_t* dE, hipStream_t s);
-hipError_t sorted_runs(const uint64_t* sorted, int64_t n, int ib, uint32_t* small, uint64_t* uniq, uint32_t* runs,
-                       uint32_t* roffs, uint32_t* dE, hipStream_t s);
 hipError_t bucket_sort_pairs(const uint64_t* keys, const uint32_t* vals, uint64_t* ktmp, uint32_t* vtmp,
                              uint64_t* kout, uint32_t* vout, int64_t n, int hi_bit, uint32_t* small, void** temp,
                              size_t* temp_bytes, hipStream_t s);
@@ -272,15 +269,6 @@ static bool bucket_sort_pairs_on(int64_t n) {
     if (e) return e[0] == '1';
     return n <= (int64_t)(32 << 20);
 }
-// runs of the onesweep-sorted keys by sorted_runs (ctg_sort.hip: count, scan,
-// write) instead of rocPRIM's run_length_encode + exclusive_scan when
-// CTG_SORTED_RUNS=1.  Parity-tested, but slower: configs[4] segment 0.98 ->
-// 1.38 ms (4085 chunks of 33 K keys, 132 barrier-separated rounds each), so
-// the library pair stays the default (profiles/r3/s3/ab_sorted_runs.jsonl)
-static bool sorted_runs_on() {
-    const char* e = getenv("CTG_SORTED_RUNS");   // read per call: tests switch it
-    return e && e[0] == '1';
-}
 static int64_t sort_wide_digits_max() {
     static const int64_t v = [] {
         const char* e = getenv("CTG_SORT_WIDE_MAX");
@@ -388,14 +376,8 @@ static hipError_t reduce_records(Workspace& w, const ReduceJob& J, hipStream_t s
         ROCPRIM_CALL(w, rocprim::radix_sort_keys<RecordSortConfig>(t, tbytes, w.sk_in, w.sk_out, (size_t)n,
                                                                    (unsigned)ib, (unsigned)(ib + ub + nb), s));
         ev.mark(3);
-        if (sorted_runs_on()) {
-            e = sorted_runs(w.sk_out, n, ib, w.bsort, w.uniq, w.runs, w.offs, dE_all, s);
-            if (e != hipSuccess) return e;
-            have_offs = true;
-        } else {
-            auto key_only = rocprim::make_transform_iterator(w.sk_out, [ib] __device__(uint64_t k) { return k >> ib; });
-            ROCPRIM_CALL(w, rocprim::run_length_encode(t, tbytes, key_only, (unsigned)n, w.uniq, w.runs, dE_all, s));
-        }
+        auto key_only = rocprim::make_transform_iterator(w.sk_out, [ib] __device__(uint64_t k) { return k >> ib; });
+        ROCPRIM_CALL(w, rocprim::run_length_encode(t, tbytes, key_only, (unsigned)n, w.uniq, w.runs, dE_all, s));
     } else if (spread && bucket_sort_pairs_on(n)) {
         // tmp buffers: w.uniq (keys) and w.keep (values) are free until the
         // run-length pass / the reduction
@@ -411,13 +393,7 @@ static hipError_t reduce_records(Workspace& w, const ReduceJob& J, hipStream_t s
     }
     if (!packed) {
         ev.mark(3);
-        if (sorted_runs_on()) {
-            e = sorted_runs(w.sk_out, n, 0, w.bsort, w.uniq, w.runs, w.offs, dE_all, s);
-            if (e != hipSuccess) return e;
-            have_offs = true;
-        } else {
-            ROCPRIM_CALL(w, rocprim::run_length_encode(t, tbytes, w.sk_out, (unsigned)n, w.uniq, w.runs, dE_all, s));
-        }
+        ROCPRIM_CALL(w, rocprim::run_length_encode(t, tbytes, w.sk_out, (unsigned)n, w.uniq, w.runs, dE_all, s));
     }
     // offsets over the n-bound: entries past E_all are never read
     if (!have_offs)
@@ -975,7 +951,7 @@ int ctg_rag_features(const void* labels, int label_bits, const void* data, int d
     P.check_planes = 8;
     if (const char* cp = getenv("CTG_CHECK_PLANES")) P.check_planes = std::max(1, atoi(cp));
     // planes per workgroup: 32, fewer where that leaves < ~1024 workgroups,
-    // 64 where even 64-plane tiles give >= 32 K workgroups (A/B with the 5/8
+    // 64 (128) where even 64 (128)-plane tiles give >= 32 K workgroups (A/B with the 5/8
     // table fill, 32 vs 64 planes: 512^3 step 1.027 -> 1.014 ms, configs[4]
     // 32.2 -> 30.0 ms with records 148 M -> 134 M; 2048^3 scan 30.4 vs 30.9 ms
     // favours 64)
@@ -983,6 +959,10 @@ int ctg_rag_features(const void* labels, int label_bits, const void* data, int d
         const int64_t rows = scan_tile_rows();
         const int64_t cols = ((shape[2] + TILE_X - 1) / TILE_X) * ((shape[1] + rows - 1) / rows);
         int tz = cols * ((shape[0] + 63) / 64) >= 32768 ? 64 : 32;
+        // 128 where even 128-plane tiles leave >= 32 K workgroups (2048^3: scan
+        // 29.76 -> 29.35 ms, records 28.1 M -> 27.3 M, step 33.65 -> 33.08 ms;
+        // profiles/r4/ablate)
+        if (cols * ((shape[0] + 127) / 128) >= 32768) tz = 128;
         while (tz > 8 && cols * ((shape[0] + tz - 1) / tz) < 1024) tz /= 2;
         if (const char* t = getenv("CTG_TILE_Z")) tz = std::max(1, atoi(t));
         P.tile_z = tz;
@@ -1024,49 +1004,7 @@ int ctg_rag_features(const void* labels, int label_bits, const void* data, int d
     for (int c = 0; c < P.n_channels; ++c)
         long_range |= std::abs(P.offsets[c][0]) + std::abs(P.offsets[c][1]) + std::abs(P.offsets[c][2]) > 1;
 
-    // Long-range affinity scans gather the partner label of every channel at
-    // p + o_c: 4-B gathers on the 8-B-strided uint64 array use half of every
-    // line they pull.  One narrowing pass (12 B / voxel) gives them -- and the
-    // graph pass and the scan's own plane loads -- a u32 copy when every label
-    // is < 2^32 (checked by the same pass; otherwise the 64-bit path and its
-    // dense relabelling run as before).  CTG_NARROW_LABELS: 1 long-range
-    // calls, 2 every affinity call; default 0 (off): measured on configs[3]
-    // 1024^3, the 12-channel scan went 45.39 -> 45.03 ms for a 2.70 ms pass,
-    // the 3-channel scan 8.91 -> 9.06 ms -- the channel loop is bound by its
-    // folds (4.2e9 samples), not by the lines the gathers pull.
-    struct DevBuf {
-        void* p = nullptr;
-        ~DevBuf() { dfree(p); }
-    } l32;
-    {
-        const char* nl = getenv("CTG_NARROW_LABELS");
-        const int mode = nl ? atoi(nl) : 0;
-        const bool want = label_bits == 64 && V > 0 && P.n_channels > 0 &&
-                          (mode == 2 || (mode == 1 && long_range)) && ((uintptr_t)dl % 16) == 0;
-        if (data) w.last_ms[7] = 0.0;   // graph-only calls (the adjacency pass) keep the caller's value
-        if (want) {
-            l32.p = dalloc((size_t)V * 4);
-            if (l32.p) {
-                CTG_CHECK(hipMemsetAsync(w.small + 16, 0, 4, s));
-                if (w.profiling) hipEventRecord(w.ev[8], s);
-                CTG_CHECK(launch_narrow_labels((const uint64_t*)dl, (uint32_t*)l32.p, V, w.small + 16, s));
-                if (w.profiling) hipEventRecord(w.ev[9], s);
-                CTG_CHECK(hipMemcpyAsync(w.small_host + 16, w.small + 16, 4, hipMemcpyDeviceToHost, s));
-                CTG_CHECK(hipStreamSynchronize(s));
-                if (w.profiling) {
-                    float nms = 0.f;
-                    hipEventElapsedTime(&nms, w.ev[8], w.ev[9]);
-                    w.last_ms[7] = nms;
-                }
-                if (w.small_host[16] == 0) {
-                    dl = l32.p;
-                    label_bits = 32;
-                    P.labels = dl;
-                    P.label_bits = 32;
-                }
-            }
-        }
-    }
+    if (data) w.last_ms[7] = 0.0;   // the narrowing pass of earlier builds: no longer run
     if (long_range && !(flags & CTG_NO_ADJ_FILTER) && V > 0) {
         rc = ctg_rag_features(dl, label_bits, nullptr, CTG_DATA_NONE, 0, nullptr, shape, own_begin, own_end, 0,
                               hist_lo, hist_hi, 0, CTG_MEM_DEVICE, stream, &adj_graph);

@@ -76,9 +76,6 @@ constexpr int NPER = CTG_NPER;                            // staged entries fold
 // u16 histogram slots: a table entry holds at most 65535 samples.  Each wave
 // folds at most this many samples between two table flushes (it requests a
 // flush before a batch would exceed it), so no entry can pass the bound.
-// u16 histogram slots: a table entry holds at most 65535 samples.  Each wave
-// folds at most this many samples between two table flushes (it requests a
-// flush before a batch would exceed it), so no entry can pass the bound.
 constexpr uint32_t WAVE_SAMPLE_BUDGET = 65535u / WAVES;
 // flush past 5/8 of the table: more live entries per flush interval, fewer
 // records (A/B over the BASELINE workloads, tools/ab_run.sh: 256 -> 320 cut
@@ -88,10 +85,6 @@ constexpr uint32_t WAVE_SAMPLE_BUDGET = 65535u / WAVES;
 #define CTG_FILL_SOFT (TABLE_CAP * 5 / 8)
 #endif
 constexpr uint32_t FILL_SOFT = CTG_FILL_SOFT;
-// poll the flush request after every fold batch (1) or only at plane ends (0)
-#ifndef CTG_POLL_AFTER_FOLD
-#define CTG_POLL_AFTER_FOLD 1
-#endif             // request a flush past this many keys
 constexpr uint32_t MARK_ADJ = 0xFFFFFFFFu;                // stage entry: nearest-neighbour face, no sample
 constexpr uint32_t MARK_ONE = 0xFFFFFFFEu;                // stage entry: one affinity sample in .z
 constexpr uint32_t MARK_ONE_ADJ = 0xFFFFFFFDu;            // ... of a nearest-neighbour face (Bloom-filtered calls)
@@ -133,9 +126,6 @@ __device__ __forceinline__ uint32_t pivot_bits(float a) { return a == a ? __floa
 // 64-bit multiply-add: bits 14.. of the product sum mix every one of the low
 // 24 bits of u and v; labels that differ only above bit 24 share buckets,
 // which costs probes, never correctness.
-#ifndef CTG_HASH24
-#define CTG_HASH24 1
-#endif
 constexpr bool TABLE_POW2 = (TABLE_CAP & (TABLE_CAP - 1)) == 0;
 // hash -> first slot of a 4-slot bucket (any table size: multiply-high)
 __device__ __forceinline__ uint32_t bucket_of(uint32_t h) {
@@ -143,16 +133,8 @@ __device__ __forceinline__ uint32_t bucket_of(uint32_t h) {
     else return __umulhi(h, (uint32_t)(TABLE_CAP / 4)) * 4u;
 }
 __device__ __forceinline__ uint32_t home_bucket(uint32_t u, uint32_t v) {
-#if CTG_HASH24
     const uint32_t p = (u & 0xFFFFFFu) * 0x9E3779u + ((v ^ (u >> 24)) & 0xFFFFFFu) * 0x85EBCBu;
     return TABLE_POW2 ? bucket_of(p >> 12) : bucket_of(p << 8);
-#else
-    uint32_t h = u * 0x9E3779B1u + v * 0x85EBCA6Bu;
-    h ^= h >> 15;
-    h *= 0x2C1B3C6Du;
-    h ^= h >> 13;
-    return bucket_of(h);
-#endif
 }
 
 // Workgroup barrier that orders LDS only.  __syncthreads() also waits for every
@@ -479,12 +461,9 @@ __device__ __forceinline__ double dpp_f64(double v) {
 #ifndef CTG_PAIR_FOLD
 #define CTG_PAIR_FOLD 1
 #endif
-// affinity maps: off -- measured slower (configs[3] 12-channel scan 45.8 ->
-// 49.9 ms, 3-channel 8.98 -> 9.84 ms): the channel loop's entries rarely
-// share a slot within a quad, and the exchanges lengthen every fold
-#ifndef CTG_PAIR_FOLD_AFF
-#define CTG_PAIR_FOLD_AFF 0
-#endif
+// (affinity maps: not grouped -- measured slower, configs[3] 12-channel scan
+// 45.8 -> 49.9 ms, 3-channel 8.98 -> 9.84 ms: the channel loop's entries
+// rarely share a slot within a quad, and the exchanges lengthen every fold)
 template <int MODE, bool FAST40, bool BATCH, typename StageT, int NPER>
 __device__ __forceinline__ void fold_grouped(Table& T, const StageT (&e)[NPER], const int (&slot)[NPER],
                                              const uint32_t (&pv)[NPER], int lane, RecordBuf R, Counters* C,
@@ -625,9 +604,8 @@ __device__ __forceinline__ void fold_batch(Table& T, const StageT* __restrict__ 
             pv[i] = __hip_atomic_load(&T.w[slot[i]][24], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
 #if CTG_PAIR_FOLD
-    // grouped atomics: whole-array boundary maps (CTG_PAIR_FOLD 1) and, A/B,
-    // affinity maps (CTG_PAIR_FOLD_AFF)
-    if constexpr ((MODE == MODE_BOUNDARY || (CTG_PAIR_FOLD_AFF && MODE == MODE_AFFINITY)) && !BATCH) {
+    // grouped atomics: whole-array boundary maps
+    if constexpr (MODE == MODE_BOUNDARY && !BATCH) {
         fold_grouped<MODE, FAST40, BATCH, StageT, NPER>(T, e, slot, pv, lane, R, C, scale, offset);
         return;
     }
@@ -877,9 +855,7 @@ __global__ __launch_bounds__(SCAN_THREADS, CTG_SCAN_MIN_WAVES) void k_face_scan(
             fold_batch<MODE, FAST40, BATCH, StageT, NP>(T, stage, nbuf, lane, R, C, scale, offset, need, ablate);
             nbuf = 0;
             if (stamps) t_fold += stamp_now() - t0;
-#if CTG_POLL_AFTER_FOLD
-            poll();
-#endif
+            poll();   // after every fold batch (only at plane ends: slower)
         }
     };
     // append the active lanes of one site to the stage
@@ -1024,10 +1000,8 @@ __global__ __launch_bounds__(SCAN_THREADS, CTG_SCAN_MIN_WAVES) void k_face_scan(
                         for (int j = 0; j < AFF_G; ++j) {
                             if (c0 + j >= P.n_channels) break;
                             const uint32_t mk = (P.bloom != nullptr && !(glr >> j & 1u)) ? MARK_ONE_ADJ : MARK_ONE;
-#ifndef CTG_PAIR_ALL
-#define CTG_PAIR_ALL 0   // 1: pair nearest-neighbour channels too (A/B: nn1024 scan 8.6 -> 9.4 ms)
-#endif
-                            if (mk == MARK_ONE && (CTG_PAIR_ALL || P.bloom != nullptr)) {
+                            // (nearest-neighbour channels unpaired: A/B nn1024 scan 8.6 -> 9.4 ms paired)
+                            if (mk == MARK_ONE && P.bloom != nullptr) {
                                 // long-range (or unfiltered) channel: lanes 2i, 2i+1 with the
                                 // same key fold as one two-sample entry (along x a cell pair
                                 // spans runs of lanes), ~halving this channel's fold work
@@ -1128,9 +1102,7 @@ static hipError_t launch_scan_r(const ScanParams& P, const RecordBuf& R, Counter
     if (nwg <= 0) return hipSuccess;
     if (nwg > 0x7FFFFFFF) return hipErrorInvalidValue;
     dim3 grid((unsigned)nwg);
-    // diagnostic: unused dynamic LDS per workgroup (CTG_SCAN_LDS_PAD bytes) lowers
-    // the workgroups resident per CU -- the scan's sensitivity to occupancy
-    static const unsigned pad = [] { const char* v = getenv("CTG_SCAN_LDS_PAD"); return v ? (unsigned)atoi(v) : 0u; }();
+    constexpr unsigned pad = 0;   // dynamic LDS
     if (P.blocks) {
         if (P.fast40)
             hipLaunchKernelGGL((k_face_scan<LabelT, DataT, MODE, true, true, NR>), grid, dim3(SCAN_THREADS), pad, s, Q,
@@ -1215,42 +1187,6 @@ hipError_t launch_density(const void* L, int label_bits, const int64_t* shape, i
     else
         hipLaunchKernelGGL(k_density<uint64_t>, dim3(n_rows), dim3(256), 0, s, (const uint64_t*)L, shape[0], shape[1],
                            shape[2], out);
-    return hipGetLastError();
-}
-
-// uint64 labels -> their low halves (long-range affinity scans gather the
-// partner label at p + o_c for every channel: from a u32 array each 64-B line
-// serves 16 labels instead of 8).  Four labels per thread (two 16-B loads,
-// one 16-B store); the OR of every high half lands in *ovf (labels >= 2^32:
-// the caller keeps the 64-bit path and its dense relabelling).
-__global__ __launch_bounds__(256) void k_narrow_labels(const uint4* __restrict__ L, uint4* __restrict__ out,
-                                                        int64_t n4, const uint64_t* __restrict__ tail_in,
-                                                        uint32_t* __restrict__ tail_out, int tail,
-                                                        uint32_t* __restrict__ ovf) {
-    uint32_t hi = 0;
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
-        const uint4 a = L[2 * i];
-        const uint4 b = L[2 * i + 1];
-        hi |= a.y | a.w | b.y | b.w;
-        out[i] = make_uint4(a.x, a.z, b.x, b.z);
-    }
-    if (blockIdx.x == 0 && (int)threadIdx.x < tail) {
-        const uint64_t l = tail_in[threadIdx.x];
-        hi |= (uint32_t)(l >> 32);
-        tail_out[threadIdx.x] = (uint32_t)l;
-    }
-    if (__ballot(hi != 0) && (threadIdx.x & (WAVE - 1)) == 0) atomicOr(ovf, 1u);
-}
-
-hipError_t launch_narrow_labels(const uint64_t* L, uint32_t* out, int64_t n, uint32_t* ovf, hipStream_t s) {
-    if (n <= 0) return hipSuccess;
-    const int64_t n4 = n / 4;
-    const int tail = (int)(n - n4 * 4);
-    int64_t grid = std::min<int64_t>((n4 + 255) / 256, 256 * 16);
-    grid = std::max<int64_t>(grid, 1);
-    hipLaunchKernelGGL(k_narrow_labels, dim3((unsigned)grid), dim3(256), 0, s, (const uint4*)L, (uint4*)out, n4,
-                       L + n4 * 4, out + n4 * 4, tail, ovf);
     return hipGetLastError();
 }
 

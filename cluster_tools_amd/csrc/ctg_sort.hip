@@ -260,91 +260,6 @@ hipError_t bucket_runs(const uint64_t* sorted, int64_t n, int lo_bit, int hi_bit
     return hipGetLastError();
 }
 
-// Runs of a fully sorted key array (onesweep output: configs[4]-sized record
-// sets, pair sorts): fixed chunks of the array play the buckets' part.  Heads
-// are global (i == 0 or a key change), so a run that crosses a chunk edge
-// belongs to the chunk holding its head, which walks past the edge for its
-// length.  Same three-launch shape as bucket_runs, in place of rocPRIM's
-// run-length encode + exclusive scan (two passes with look-back state).
-__device__ __forceinline__ bool is_head_g(const uint64_t* k, uint32_t i, int ib) {
-    return i == 0 || (k[i] >> ib) != (k[i - 1] >> ib);
-}
-
-__global__ __launch_bounds__(BK_THREADS) void k_sorted_heads_count(const uint64_t* __restrict__ keys, uint32_t n,
-                                                                   int ib, uint32_t chunk, uint32_t* __restrict__ hc) {
-    __shared__ uint32_t red[BK_THREADS / 64];
-    const uint32_t b0 = blockIdx.x * chunk, b1 = min(n, b0 + chunk);
-    uint32_t c = 0;
-    for (uint32_t i = b0 + threadIdx.x; i < b1; i += BK_THREADS) c += is_head_g(keys, i, ib) ? 1u : 0u;
-    for (int o = 32; o > 0; o >>= 1) c += (uint32_t)__shfl_xor((int)c, o, 64);
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = c;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        uint32_t t = 0;
-        for (int w = 0; w < BK_THREADS / 64; ++w) t += red[w];
-        hc[blockIdx.x] = t;
-    }
-}
-
-__global__ __launch_bounds__(BK_THREADS) void k_sorted_heads_write(const uint64_t* __restrict__ keys, uint32_t n,
-                                                                   int ib, uint32_t chunk, uint32_t nch,
-                                                                   const uint32_t* __restrict__ ho,
-                                                                   uint64_t* __restrict__ uniq,
-                                                                   uint32_t* __restrict__ runs,
-                                                                   uint32_t* __restrict__ roffs,
-                                                                   uint32_t* __restrict__ dE) {
-    __shared__ uint32_t wsum[BK_THREADS / 64];
-    const uint32_t b0 = blockIdx.x * chunk, b1 = min(n, b0 + chunk);
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    if (blockIdx.x == 0 && threadIdx.x == 0) *dE = ho[nch];
-    uint32_t base = ho[blockIdx.x];
-    for (uint32_t c0 = b0; c0 < b1; c0 += BK_THREADS) {
-        const uint32_t i = c0 + threadIdx.x;
-        const bool h = i < b1 && is_head_g(keys, i, ib);
-        const uint64_t m = __ballot(h);
-        const uint32_t r = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
-        if (lane == 0) wsum[wv] = (uint32_t)__popcll(m);
-        __syncthreads();
-        uint32_t before = 0, total = 0;
-#pragma unroll
-        for (int w = 0; w < BK_THREADS / 64; ++w) {
-            before += w < wv ? wsum[w] : 0u;
-            total += wsum[w];
-        }
-        if (h) {
-            const uint32_t e = base + before + r;
-            const uint64_t k = keys[i] >> ib;
-            uint32_t j = i + 1;
-            while (j < n && (keys[j] >> ib) == k) ++j;   // runs are short (~2 records per edge)
-            uniq[e] = k;
-            roffs[e] = i;
-            runs[e] = j - i;
-        }
-        base += total;
-        __syncthreads();
-    }
-}
-
-// sorted keys (key bits from ib up) -> uniq keys (>> ib), run lengths, run
-// offsets, *dE = number of runs.  small: the BK_SMALL_WORDS bucket scratch.
-hipError_t sorted_runs(const uint64_t* sorted, int64_t n, int ib, uint32_t* small, uint64_t* uniq, uint32_t* runs,
-                       uint32_t* roffs, uint32_t* dE, hipStream_t s) {
-    if (n <= 0) return hipSuccess;
-    if (n > 0xFFFFFFFFll) return hipErrorInvalidValue;
-    constexpr uint32_t M = 1u << BK_MAX_BITS;
-    // at most M chunks, each a multiple of the workgroup, at least 16 rounds
-    uint32_t chunk = (uint32_t)((n + M - 1) / M);
-    chunk = std::max<uint32_t>(16 * BK_THREADS, (chunk + BK_THREADS - 1) / BK_THREADS * BK_THREADS);
-    const uint32_t nch = (uint32_t)((n + chunk - 1) / chunk);
-    uint32_t* hc = small + 2 * M + 1;
-    uint32_t* ho = small + 3 * M + 1;
-    hipLaunchKernelGGL(k_sorted_heads_count, dim3(nch), dim3(BK_THREADS), 0, s, sorted, (uint32_t)n, ib, chunk, hc);
-    hipLaunchKernelGGL(k_bucket_scan, dim3(1), dim3(1024), 0, s, hc, nch, ho, small + 4 * M + 2);
-    hipLaunchKernelGGL(k_sorted_heads_write, dim3(nch), dim3(BK_THREADS), 0, s, sorted, (uint32_t)n, ib, chunk, nch,
-                       ho, uniq, runs, roffs, dE);
-    return hipGetLastError();
-}
-
 // keys (n, packed: key bits [lo_bit, hi_bit), slot bits below) -> sorted by
 // the key bits into out (order among equal keys: any).  tmp: n u64;
 // small: 3 * 4096 + 1 u32; temp / temp_bytes: the caller's growable scratch.

@@ -504,28 +504,3 @@ def test_bucket_sort_skewed_keys(gpu, monkeypatch):
     e_o, f_o = O.boundary_features(lab, bnd)
     np.testing.assert_array_equal(out['edges'], e_o)
     check_features(out['features'], f_o)
-
-
-@pytest.mark.parametrize('packed', ['0', '1'])
-def test_sorted_runs_match_library_rle(gpu, monkeypatch, packed):
-    """Run extraction after the onesweep sort (ctg_sort.hip sorted_runs: heads
-    per fixed chunk, runs that cross a chunk edge walked by their head's
-    chunk) against rocPRIM's run-length encode + exclusive scan
-    (CTG_SORTED_RUNS=0) and the oracle; packed keys (slot bits below the key)
-    and the unpacked (key, slot) pair path, both forced off the bucket sort.
-    Cell 3 on 40 x 96 x 128 voxels: ~121 K edges, tens of 4096-key chunks."""
-    lab, bnd = S.generate((40, 96, 128), cell=3, seed=12)
-    monkeypatch.setenv('CTG_BUCKET_SORT', '0')
-    monkeypatch.setenv('CTG_BUCKET_SORT_PAIRS', '0')
-    monkeypatch.setenv('CTG_SORT_PACKED', packed)
-    monkeypatch.setenv('CTG_SORTED_RUNS', '1')
-    out = rag.rag_features(lab, bnd)
-    monkeypatch.setenv('CTG_SORTED_RUNS', '0')
-    ref = rag.rag_features(lab, bnd)
-    np.testing.assert_array_equal(out['edges'], ref['edges'])
-    np.testing.assert_array_equal(out['nodes'], ref['nodes'])
-    np.testing.assert_array_equal(out['features'][:, 9], ref['features'][:, 9])
-    np.testing.assert_allclose(out['features'], ref['features'], rtol=1e-12, atol=1e-15)
-    e_o, f_o = O.boundary_features(lab, bnd)
-    np.testing.assert_array_equal(out['edges'], e_o)
-    check_features(out['features'], f_o)
