@@ -170,6 +170,43 @@ def _config0_write_inputs(path, shape, block, cell, seed):
     return sum(os.path.getsize(os.path.join(r, fn)) for r, _, fs in os.walk(path) for fn in fs)
 
 
+def cpu_baseline_config0(inp, tmpdir, shape, block, workers):
+    """configs[0] CPU baseline: the per-block job bodies (gzip N5 ROI reads,
+    RAG + 10 features of every block on the scalar C restatement, varlength
+    gzip chunk writes of nodes / edges / sub_features) over the same N5 input,
+    one single-threaded job per worker process (blocks dealt k::workers, as
+    LocalTask deals them); value = voxels / the slowest job (all at once).  The
+    merge tasks (one job each) are not included."""
+    import multiprocessing as mp
+    import shutil
+    from concurrent.futures import ProcessPoolExecutor
+    from oracle import c_oracle
+    from cluster_tools_amd import n5
+    from cluster_tools_amd.blocking import blocking
+    nb = blocking([0, 0, 0], list(shape), list(block)).numberOfBlocks
+    workers = max(1, min(workers, nb))
+    best = None
+    for rep in range(2):
+        out = os.path.join(tmpdir, 'cpu%d.n5' % rep)
+        with n5.File(out) as fo:
+            for k in ('s0/sub_graphs/nodes', 's0/sub_graphs/edges'):
+                fo.require_dataset(k, shape=list(shape), chunks=list(block), compression='gzip', dtype='uint64')
+            fo.require_dataset('s0/sub_features', shape=list(shape), chunks=list(block), compression='gzip',
+                               dtype='float64')
+        jobs = [(inp, out, list(block), list(range(nb))[k::workers]) for k in range(workers)]
+        with ProcessPoolExecutor(workers, mp_context=mp.get_context('spawn')) as ex:
+            res = list(ex.map(c_oracle.block_job, jobs))
+        shutil.rmtree(out, ignore_errors=True)
+        t = max(r[1] for r in res)
+        best = t if best is None else min(best, t)
+    V = int(np.prod(shape))
+    return {'value': round(V / best / 1e9, 6), 'unit': 'Gvoxels/s', 'cores': workers, 'kind': 'port',
+            'sample': 'the whole configs[0] volume (%dx%dx%d, %d blocks of %s): per-block job bodies (gzip N5 ROI '
+                      'reads, RAG + features on oracle/ctg_oracle.c, varlength gzip writes of nodes / edges / '
+                      'sub_features) on %d single-threaded worker processes, %.2f s slowest job (best of 2); '
+                      'merge tasks not included' % (tuple(shape) + (nb, 'x'.join(map(str, block)), workers, best))}
+
+
 # Job processes per task in process mode.  'gpu': one job per task -- each job
 # is a GPU process, and creating / tearing down a device context costs ~60 ms
 # that the driver serialises across processes (15 graph jobs exit in ~0.9 s),
@@ -207,6 +244,10 @@ def bench_config0(args):
             in_bytes = ex.submit(_config0_write_inputs, inp, shape, block, cell, args.seed).result()
 
         def step(k, mode, jobs):
+            # every step starts from cold decode caches (thread mode: the bench
+            # process's cache would otherwise still hold the input of the last step)
+            from cluster_tools_amd import _lib
+            _lib.load().ctg_io_cache_clear()
             out = os.path.join(d, 'out%d.n5' % k)
             t = workflow.graph_workflow(inp, 'seg', out, 'graph', block, max_jobs=jobs['graph'], mode=mode)
             workflow.edge_features_workflow(inp, 'bnd', inp, 'seg', out, 'graph', out, 'features', block,
@@ -255,6 +296,7 @@ def bench_config0(args):
         proc_split_c = split()
         ms_t, stages_t, feat_prof, _ = measure('threads', dict(graph=16, features=1, merge=4), 1000)
 
+        cpu = None if args.no_cpu_baseline else cpu_baseline_config0(inp, d, shape, block, args.cpu_threads)
         from cluster_tools_amd import _lib, n5, rag
         from cluster_tools_amd.blocking import blocking
         torch.cuda.set_device(0 if args.device is None else args.device)
@@ -342,7 +384,7 @@ def bench_config0(args):
                      'achieved': round(alg / (scan_avg * 1e-3) / 1e9, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                      'frac': round(alg / (scan_avg * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), 'traffic': traffic,
                      'traffic_source': traffic_src},
-        'cpu_baseline': None,
+        'cpu_baseline': cpu,
     }
     print(json.dumps(line), flush=True)
 

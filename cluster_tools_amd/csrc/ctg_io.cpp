@@ -319,9 +319,13 @@ struct CacheEntry {
     std::list<std::string>::iterator lru;
 };
 
-std::mutex g_cache_mu;
-std::unordered_map<std::string, CacheEntry> g_cache;
-std::list<std::string> g_lru;   // front = most recently used (ready entries only)
+// The cache and the readahead pool are never destroyed: a drop-in job process
+// ends right after its last call, and tearing down GBs of decoded chunks (one
+// munmap per chunk, each a TLB shootdown across the pool's threads) or joining
+// threads in the middle of a decode only delays the exit (the OS reclaims it).
+std::mutex& g_cache_mu = *new std::mutex;
+std::unordered_map<std::string, CacheEntry>& g_cache = *new std::unordered_map<std::string, CacheEntry>;
+std::list<std::string>& g_lru = *new std::list<std::string>;   // front = most recently used (ready entries only)
 size_t g_cache_bytes = 0;
 
 size_t cache_budget() {
@@ -487,9 +491,9 @@ ChunkPtr get_chunk(const std::string& path, int format, int ndim, const int64_t*
 // ---------------------------------------------------------------------------
 class Prefetcher {
 public:
-    static Prefetcher& get() {   // function-local: destroyed before the cache globals
-        static Prefetcher p;
-        return p;
+    static Prefetcher& get() {   // never destroyed (see g_cache): no join at process exit
+        static Prefetcher* p = new Prefetcher;
+        return *p;
     }
     void submit(std::function<void()> f) {
         {

@@ -83,3 +83,45 @@ def chunk_job(args):
     t0 = time.perf_counter()
     e, _ = features(lab, dat, own_begin=(halo, 0, 0))
     return int(e.shape[0]), time.perf_counter() - t0
+
+
+def block_job(args):
+    """configs[0] CPU baseline (bench.py): the per-block job bodies of the
+    reference's local target on the scalar C restatement, with the same gzip
+    N5 I/O -- for every block of the job: read the labels and boundary ROIs
+    (block + lower halo, increaseRoi, initial_sub_graphs.py:124-129 /
+    block_edge_features.py:127-134) from the N5 input, compute the RAG and the
+    10 features of the block's owned faces, write the block's varlength
+    ``nodes`` / ``edges`` / ``sub_features`` chunks (gzip).  One
+    single-threaded job per worker process, as LocalTask runs it
+    (cluster_tasks.py:528-550).  args = (input path, output path, block shape,
+    block ids) -> (n_edges, seconds of the job body)."""
+    import time
+    import numpy as np
+    from cluster_tools_amd import n5
+    from cluster_tools_amd.blocking import blocking
+    inp, out, block_shape, block_ids = args
+    load()
+    t0 = time.perf_counter()
+    n_edges = 0
+    with n5.File(inp, 'r') as f, n5.File(out) as fo:
+        ds_l, ds_d = f['seg'], f['bnd']
+        shape = list(ds_l.shape)
+        blk = blocking([0, 0, 0], shape, list(block_shape))
+        g_nodes, g_edges, g_feat = fo['s0/sub_graphs/nodes'], fo['s0/sub_graphs/edges'], fo['s0/sub_features']
+        for b in block_ids:
+            bb = blk.getBlock(b)
+            rb = [max(x - 1, 0) for x in bb.begin]
+            sl = tuple(slice(x, y) for x, y in zip(rb, bb.end))
+            lab = np.ascontiguousarray(ds_l[sl], dtype=np.uint64)
+            dat = np.ascontiguousarray(ds_d[sl], dtype=np.float32)
+            own = tuple(x - r for x, r in zip(bb.begin, rb))
+            e, ft = features(lab, dat, own_begin=own)
+            inner = lab[tuple(slice(o, None) for o in own)]
+            pos = blk.blockGridPosition(b)
+            g_nodes.write_chunk(pos, np.unique(inner), True)
+            if e.shape[0]:
+                g_edges.write_chunk(pos, e.ravel(), True)
+                g_feat.write_chunk(pos, ft.ravel(), True)
+            n_edges += e.shape[0]
+    return n_edges, time.perf_counter() - t0
