@@ -85,6 +85,8 @@ constexpr uint32_t WAVE_SAMPLE_BUDGET = 65535u / WAVES;
 #define CTG_FILL_SOFT (TABLE_CAP * 5 / 8)
 #endif
 constexpr uint32_t FILL_SOFT = CTG_FILL_SOFT;
+// (the inserting lane compares the returned fill count: non-returning
+// increments checked at every poll measured slower, 2048^3 scan 29.38 -> 29.92 ms)
 constexpr uint32_t MARK_ADJ = 0xFFFFFFFFu;                // stage entry: nearest-neighbour face, no sample
 constexpr uint32_t MARK_ONE = 0xFFFFFFFEu;                // stage entry: one affinity sample in .z
 constexpr uint32_t MARK_ONE_ADJ = 0xFFFFFFFDu;            // ... of a nearest-neighbour face (Bloom-filtered calls)
@@ -453,21 +455,25 @@ __device__ __forceinline__ double dpp_f64(double v) {
 // Boundary-map fold with same-key lanes combined first.  Faces of one site
 // arrive in x order, so runs of lanes hold the same key (a cell pair's y / z
 // boundary spans several voxels along x); their LDS atomics to one entry
-// serialise in the LDS banks.  Within each aligned lane pair, then quad, lanes
-// that resolved to the same table slot add their shifted sums and fold their
-// min / max with two DPP exchanges, and only the group's first lane issues
-// the sum / sum-of-squares / min / max atomics (the histogram adds stay per
-// lane: two samples rarely share a slot word with their neighbours').
+// serialise in the LDS banks.  Within each aligned lane pair, lanes that
+// resolved to the same table slot add their shifted sums and fold their min /
+// max with one DPP exchange, and only the pair's first lane issues the sum /
+// sum-of-squares / min / max atomics (the histogram adds stay per lane: two
+// samples rarely share a slot word with their neighbours').  Pairs only: a
+// second (quad) stage cost more issue than its saved atomics (scan 2048^3
+// 29.92 -> 29.43 ms, 512^3 0.756 -> 0.710, configs[4] 14.63 -> 14.23;
+// profiles/r4/e).
 #ifndef CTG_PAIR_FOLD
 #define CTG_PAIR_FOLD 1
 #endif
+
 // (affinity maps: not grouped -- measured slower, configs[3] 12-channel scan
 // 45.8 -> 49.9 ms, 3-channel 8.98 -> 9.84 ms: the channel loop's entries
 // rarely share a slot within a quad, and the exchanges lengthen every fold)
 template <int MODE, bool FAST40, bool BATCH, typename StageT, int NPER>
 __device__ __forceinline__ void fold_grouped(Table& T, const StageT (&e)[NPER], const int (&slot)[NPER],
                                              const uint32_t (&pv)[NPER], int lane, RecordBuf R, Counters* C,
-                                             double scale, double offset) {
+                                             double scale, double offset, int ablate) {
     constexpr bool BND = MODE == MODE_BOUNDARY;
     constexpr bool AFF = MODE == MODE_AFFINITY;
 #pragma unroll
@@ -481,12 +487,16 @@ __device__ __forceinline__ void fold_grouped(Table& T, const StageT (&e)[NPER], 
         const bool adj = (AFF || BATCH) && e[i].w == MARK_ADJ && (AFF || e[i].z == MARK_ADJ);
         if (sl >= 0 && adj) atomicOr(&T.w[sl][21], ADJ_FLAG);
         const bool v = sl >= 0 && !adj;
+        if (ablate & 64) {   // diagnostic: probe only (slot and pivot resolved, no statistics)
+            if (v && pv[i] == 0x12345u) atomicAdd(&C->pad[1], 1ull);
+            continue;
+        }
         // affinity entries carry one sample (.w a marker) or two (.w the second)
         const bool two = BND || (AFF && e[i].w < MARK_ONE_ADJ);
         const float a = __uint_as_float(e[i].z);
         const float b = two ? __uint_as_float(e[i].w) : a;
         const double da = (double)a, db = (double)b;
-        if (v) {
+        if (v && !(ablate & 128)) {   // (diagnostic 128: no histogram)
             const int sa = sample_slot<FAST40>(da, scale, offset);
             if (two) hist_add2(T, sl, sa, sample_slot<FAST40>(db, scale, offset));
             else atomicAdd(&T.w[sl][sa >> 1], 1u << ((sa & 1) * 16));
@@ -506,7 +516,8 @@ __device__ __forceinline__ void fold_grouped(Table& T, const StageT (&e)[NPER], 
         uint32_t nnf = (AFF && v && e[i].w == MARK_ONE_ADJ) ? 1u : 0u;
         // groups: every lane active here (no divergent branch encloses this);
         // a lane without a slot gets a key no other lane has
-        const uint32_t key = v ? (uint32_t)sl : 0x80000000u | (uint32_t)lane;
+        // (diagnostic 1024: no grouping -- every lane its own atomics)
+        const uint32_t key = (v && !(ablate & 1024)) ? (uint32_t)sl : 0x80000000u | (uint32_t)lane;
         const bool g1 = dpp_x1(key) == key;
         {
             const double s1 = dpp_f64<1>(sm), q1 = dpp_f64<1>(sq);
@@ -517,22 +528,8 @@ __device__ __forceinline__ void fold_grouped(Table& T, const StageT (&e)[NPER], 
             mx = g1 ? max(mx, mx1) : mx;
             nnf = g1 ? nnf | f1 : nnf;
         }
-        // both exchanges unconditional: under a short-circuit && the compiler
-        // runs a DPP with part of the wave masked off, and a masked source
-        // lane reads as the destination's own value
-        const uint32_t g1_x2 = dpp_x2(g1 ? 1u : 0u), key_x2 = dpp_x2(key);
-        const bool g2 = g1 & (g1_x2 != 0u) & (key_x2 == key);
-        {
-            const double s2 = dpp_f64<2>(sm), q2 = dpp_f64<2>(sq);
-            const uint32_t mn2 = dpp_x2(mn), mx2 = dpp_x2(mx), f2 = AFF ? dpp_x2(nnf) : 0u;
-            sm = g2 ? sm + s2 : sm;
-            sq = g2 ? sq + q2 : sq;
-            mn = g2 ? min(mn, mn2) : mn;
-            mx = g2 ? max(mx, mx2) : mx;
-            nnf = g2 ? nnf | f2 : nnf;
-        }
-        const bool lead = !(g1 && (lane & 1)) && !(g2 && (lane & 2));
-        if (v && lead) {
+        const bool lead = !(g1 && (lane & 1));
+        if (v && lead && !(ablate & 2048)) {   // (diagnostic 2048: no moment / min / max atomics)
             atomicMin(&T.w[sl][22], mn);
             atomicMax(&T.w[sl][23], mx);
             if (AFF && nnf) atomicOr(&T.w[sl][21], ADJ_FLAG);
@@ -606,7 +603,7 @@ __device__ __forceinline__ void fold_batch(Table& T, const StageT* __restrict__ 
 #if CTG_PAIR_FOLD
     // grouped atomics: whole-array boundary maps
     if constexpr (MODE == MODE_BOUNDARY && !BATCH) {
-        fold_grouped<MODE, FAST40, BATCH, StageT, NPER>(T, e, slot, pv, lane, R, C, scale, offset);
+        fold_grouped<MODE, FAST40, BATCH, StageT, NPER>(T, e, slot, pv, lane, R, C, scale, offset, ablate);
         return;
     }
 #endif
@@ -1029,6 +1026,11 @@ __global__ __launch_bounds__(SCAN_THREADS, CTG_SCAN_MIN_WAVES) void k_face_scan(
                 }
             }
             // z faces (z, z+1): plane z against the prefetched plane
+            if (stamps) {   // diagnostic: how long the prefetched plane keeps this wave waiting
+                const uint64_t tw = stamp_now();
+                __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
+                t_wait += stamp_now() - tw;
+            }
             if ((s_zo | s_zg) && (!AFF || adj_marks)) {
 #pragma unroll
                 for (int r = 0; r < ROWS; ++r) {
