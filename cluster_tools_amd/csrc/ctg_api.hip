@@ -267,6 +267,8 @@ static bool bucket_sort() {
 static bool bucket_sort_pairs_on(int64_t n) {
     const char* e = getenv("CTG_BUCKET_SORT_PAIRS");
     if (e) return e[0] == '1';
+    // up to ~32 M records (configs[4]'s 138 M: onesweep 6.7 ms against 9.3 ms for the bucket pass with
+    // the in-LDS sort of ~34 K-record buckets split into sub-buckets; profiles/r4/g)
     return n <= (int64_t)(32 << 20);
 }
 static int64_t sort_wide_digits_max() {
@@ -358,6 +360,7 @@ static hipError_t reduce_records(Workspace& w, const ReduceJob& J, hipStream_t s
     if (e != hipSuccess) return e;
     ev.mark(2);
     bool have_offs = false;   // run offsets already written (bucket path)
+    bool pairs_done = false;  // pair sort + runs done by the bucket path
     // the bucket pass needs keys spread over their top bits: block-tagged keys
     // (ctg_rag_blocks, J.ub set) put the block id there and fill a few huge
     // buckets (configs[0] device time 3.9 -> 6.7 ms), so they keep onesweep
@@ -384,6 +387,12 @@ static hipError_t reduce_records(Workspace& w, const ReduceJob& J, hipStream_t s
         e = bucket_sort_pairs(w.sk_in, w.idx_in, w.uniq, w.keep, w.sk_out, w.idx_out, n, ub + nb, w.bsort, &w.temp,
                               &w.temp_bytes, s);
         if (e != hipSuccess) return e;
+        ev.mark(3);
+        // runs never cross the MSD buckets: unique keys, lengths and offsets per bucket
+        e = bucket_runs(w.sk_out, n, 0, ub + nb, w.bsort, w.uniq, w.runs, w.offs, dE_all, s);
+        if (e != hipSuccess) return e;
+        have_offs = true;
+        pairs_done = true;
     } else if (n <= sort_wide_digits_max()) {
         ROCPRIM_CALL(w, rocprim::radix_sort_pairs<RecordSortConfig>(t, tbytes, w.sk_in, w.sk_out, w.idx_in,
                                                                     w.idx_out, (size_t)n, 0u, (unsigned)(ub + nb), s));
@@ -391,7 +400,7 @@ static hipError_t reduce_records(Workspace& w, const ReduceJob& J, hipStream_t s
         ROCPRIM_CALL(w, rocprim::radix_sort_pairs(t, tbytes, w.sk_in, w.sk_out, w.idx_in, w.idx_out, (size_t)n, 0u,
                                                   (unsigned)(ub + nb), s));
     }
-    if (!packed) {
+    if (!packed && !pairs_done) {
         ev.mark(3);
         ROCPRIM_CALL(w, rocprim::run_length_encode(t, tbytes, w.sk_out, (unsigned)n, w.uniq, w.runs, dE_all, s));
     }

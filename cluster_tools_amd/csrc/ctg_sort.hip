@@ -19,6 +19,7 @@
 // sort's large-segment path, so there is no size precondition.
 #include <algorithm>
 
+#include <rocprim/block/block_radix_sort.hpp>
 #include <rocprim/device/device_segmented_radix_sort.hpp>
 
 #include "ctg_internal.h"
@@ -134,6 +135,158 @@ __global__ __launch_bounds__(BK_THREADS) void k_bucket_scatter_pairs(const uint6
     }
 }
 
+// ---------------------------------------------------------------------------
+// In-LDS bucket sort: after the MSD bucket pass, one workgroup per bucket
+// sorts it in LDS (rocPRIM's block radix sort: 1024 threads x 8 items), so
+// the keys make one HBM round trip after the bucket scatter.  A bucket of
+// more than LS_CAP items is first split by its next key bits into
+// sub-buckets (LDS histogram, scattered into the output range), each then
+// sorted in LDS in place; a sub-bucket still above LS_CAP (heavy skew: one
+// label adjacent to very many) raises *flag and the caller re-sorts with
+// rocPRIM's device sort.  (key, value) pairs travel as one 64-bit item:
+// (key bits below the bucket / sub-bucket bits) << 32 | value -- at most 32
+// key bits remain, the sub-bucket split guarantees it.
+// ---------------------------------------------------------------------------
+constexpr int LS_IPT = 8;
+constexpr int LS_MAX_SUB_BITS = 10;
+template <int TH>
+struct LsShared {
+    typename rocprim::block_radix_sort<uint64_t, TH, LS_IPT>::storage_type sort;
+    uint32_t cnt[1 << LS_MAX_SUB_BITS];          // sub-bucket counts, then cursors
+    uint32_t off[(1 << LS_MAX_SUB_BITS) + 1];    // sub-bucket offsets
+};
+
+// item -> (key, value) and back; KEYS: the item is the key itself
+template <bool PAIRS>
+__device__ __forceinline__ uint64_t ls_item(uint64_t k, uint32_t v, int rem) {
+    return PAIRS ? ((k & ((1ull << rem) - 1ull)) << 32) | v : k;
+}
+
+// sort items [i0, i0 + n) of (kin, vin) by key bits [lo, hi) of the item
+// into (kout, vout) at the same positions; prefix = the key bits above `rem`
+template <bool PAIRS, int TH>
+__device__ void ls_sort_range(LsShared<TH>& sh, const uint64_t* kin, const uint32_t* vin, uint64_t* kout,
+                              uint32_t* vout, uint32_t i0, uint32_t n, int rem, uint64_t prefix, int lo_bit) {
+    uint64_t it[LS_IPT];
+    const uint32_t t = threadIdx.x;
+    using LdsSort = rocprim::block_radix_sort<uint64_t, TH, LS_IPT>;
+#pragma unroll
+    for (int j = 0; j < LS_IPT; ++j) {
+        const uint32_t i = t * LS_IPT + j;
+        it[j] = i < n ? ls_item<PAIRS>(kin[i0 + i], PAIRS ? vin[i0 + i] : 0u, rem) : ~0ull;
+    }
+    // PAIRS: sort on the item bits [32, 32 + rem); KEYS: on [lo_bit, rem)
+    const unsigned b0 = PAIRS ? 32u : (unsigned)lo_bit, b1 = PAIRS ? 32u + (unsigned)rem : (unsigned)rem;
+    if (b1 > b0) LdsSort().sort(it, sh.sort, b0, b1);
+#pragma unroll
+    for (int j = 0; j < LS_IPT; ++j) {
+        const uint32_t i = t * LS_IPT + j;
+        if (i < n) {
+            if constexpr (PAIRS) {
+                kout[i0 + i] = prefix | (it[j] >> 32);
+                vout[i0 + i] = (uint32_t)it[j];
+            } else {
+                kout[i0 + i] = it[j];
+            }
+        }
+    }
+    __syncthreads();   // the shared storage is reused by the next range
+}
+
+// one workgroup per bucket of the MSD pass (offs: bucket ranges in kin);
+// key bits [lo_bit, shift) are sorted (KEYS: slot bits below lo_bit ride along)
+template <bool PAIRS, int TH>
+__global__ __launch_bounds__(TH) void k_bucket_lds_sort(const uint64_t* __restrict__ kin,
+                                                                const uint32_t* __restrict__ vin,
+                                                                uint64_t* __restrict__ kout,
+                                                                uint32_t* __restrict__ vout,
+                                                                const uint32_t* __restrict__ offs, int lo_bit,
+                                                                int shift, uint32_t* __restrict__ flag) {
+    constexpr uint32_t LS_CAP = TH * LS_IPT;
+    __shared__ LsShared<TH> sh;
+    const uint32_t b = blockIdx.x, b0 = offs[b], n = offs[b + 1] - b0;
+    if (n == 0) return;
+    const uint64_t bucket_prefix = (uint64_t)b << shift;
+    // sub-bucket bits: enough for ~LS_CAP / 2 items per sub-bucket, and (pairs)
+    // enough that at most 32 key bits remain below them
+    int sb = 0;
+    while (sb < LS_MAX_SUB_BITS && sb < shift - lo_bit && (n >> sb) > LS_CAP / 2) ++sb;
+    if (n <= LS_CAP) sb = 0;
+    if (PAIRS) sb = max(sb, shift - 32);
+    if (sb > LS_MAX_SUB_BITS || (sb > 0 && sb > shift - lo_bit)) {
+        if (threadIdx.x == 0) atomicOr(flag, 1u);
+        return;
+    }
+    if (sb == 0) {
+        ls_sort_range<PAIRS, TH>(sh, kin, vin, kout, vout, b0, n, shift, bucket_prefix, lo_bit);
+        return;
+    }
+    // split by key bits [shift - sb, shift) into kout / vout (order within a
+    // sub-bucket: any), then sort every sub-bucket in place
+    const int rem = shift - sb;
+    const uint32_t nsub = 1u << sb, smask = nsub - 1u;
+    for (uint32_t i = threadIdx.x; i < nsub; i += TH) sh.cnt[i] = 0;
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < n; i += TH)
+        atomicAdd(&sh.cnt[(uint32_t)(kin[b0 + i] >> rem) & smask], 1u);
+    __syncthreads();
+    if (threadIdx.x == 0) {   // exclusive prefix (nsub <= 1024: one thread is enough)
+        uint32_t acc = 0;
+        for (uint32_t i = 0; i < nsub; ++i) {
+            sh.off[i] = acc;
+            acc += sh.cnt[i];
+            sh.cnt[i] = 0;
+        }
+        sh.off[nsub] = acc;
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < n; i += TH) {
+        const uint64_t k = kin[b0 + i];
+        const uint32_t sbk = (uint32_t)(k >> rem) & smask;
+        const uint32_t d = b0 + sh.off[sbk] + atomicAdd(&sh.cnt[sbk], 1u);
+        kout[d] = k;
+        if constexpr (PAIRS) vout[d] = vin[b0 + i];
+    }
+    __syncthreads();
+    for (uint32_t q = 0; q < nsub; ++q) {
+        const uint32_t s0 = sh.off[q], m = sh.off[q + 1] - s0;   // uniform
+        if (m > LS_CAP) {
+            if (threadIdx.x == 0) atomicOr(flag, 1u);
+            return;
+        }
+        if (m > 1)   // (a single item is in place already)
+            ls_sort_range<PAIRS, TH>(sh, kout, vout, kout, vout, b0 + s0, m, rem,
+                                     bucket_prefix | ((uint64_t)q << rem), lo_bit);
+    }
+}
+
+// the in-LDS sort of every bucket of an MSD pass (offs: nbk + 1 bucket bounds
+// in kin); *flag (device u32) set -> some sub-bucket exceeded the LDS capacity
+template <bool PAIRS>
+static hipError_t bucket_lds_sort(const uint64_t* kin, const uint32_t* vin, uint64_t* kout, uint32_t* vout,
+                                  const uint32_t* offs, uint32_t nbk, int64_t n, int lo_bit, int shift,
+                                  uint32_t* flag, hipStream_t s) {
+    hipError_t e = hipMemsetAsync(flag, 0, 4, s);
+    if (e != hipSuccess) return e;
+    if (n / nbk <= 1024)   // small buckets: 256-thread workgroups (2 K items each in LDS)
+        hipLaunchKernelGGL((k_bucket_lds_sort<PAIRS, 256>), dim3(nbk), dim3(256), 0, s, kin, vin, kout, vout, offs,
+                           lo_bit, shift, flag);
+    else
+        hipLaunchKernelGGL((k_bucket_lds_sort<PAIRS, 1024>), dim3(nbk), dim3(1024), 0, s, kin, vin, kout, vout,
+                           offs, lo_bit, shift, flag);
+    return hipGetLastError();
+}
+
+// CTG_LDS_SORT (read per call: tests and A/B switch it): 1 in-LDS bucket sort
+// for keys and pairs, 0 rocPRIM's segmented sort of the buckets; unset: the
+// in-LDS sort for (key, slot) pairs (2048^3: sort 1.80 -> 1.54 ms), rocPRIM's
+// for packed keys (512^3: 0.074 vs 0.113 ms in LDS; profiles/r4/g)
+static bool lds_sort_on(bool pairs) {
+    const char* e = getenv("CTG_LDS_SORT");
+    if (e) return e[0] == '1';
+    return pairs;
+}
+
 static int bucket_bits(int64_t n, int key_bits) {
     int bb = 1;
     while (bb < BK_MAX_BITS && (n >> (bb + 10)) > 0) ++bb;   // ~1 K keys per bucket
@@ -163,6 +316,15 @@ hipError_t bucket_sort_pairs(const uint64_t* keys, const uint32_t* vals, uint64_
     if (shift <= 0) {
         e = hipMemcpyAsync(kout, ktmp, (size_t)n * 8, hipMemcpyDeviceToDevice, s);
         return e != hipSuccess ? e : hipMemcpyAsync(vout, vtmp, (size_t)n * 4, hipMemcpyDeviceToDevice, s);
+    }
+    if (lds_sort_on(true)) {
+        uint32_t* flag = small + 5 * (1 << BK_MAX_BITS) + 8;
+        e = bucket_lds_sort<true>(ktmp, vtmp, kout, vout, offs, nbk, n, 0, shift, flag, s);
+        if (e != hipSuccess) return e;
+        uint32_t f = 0;
+        if ((e = hipMemcpyAsync(&f, flag, 4, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
+        if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
+        if (!f) return hipSuccess;   // (else: skewed buckets -- the segmented sort below redoes all)
     }
     size_t need = 0;
     e = rocprim::segmented_radix_sort_pairs(nullptr, need, ktmp, kout, vtmp, vout, (unsigned)n, nbk, offs, offs + 1,
@@ -282,6 +444,15 @@ hipError_t bucket_sort_keys(const uint64_t* keys, uint64_t* tmp, uint64_t* out, 
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (shift <= lo_bit) {   // the buckets are the keys: already grouped and ordered
         return hipMemcpyAsync(out, tmp, (size_t)n * 8, hipMemcpyDeviceToDevice, s);
+    }
+    if (lds_sort_on(false)) {
+        uint32_t* flag = small + 5 * (1 << BK_MAX_BITS) + 8;
+        e = bucket_lds_sort<false>(tmp, nullptr, out, nullptr, offs, nbk, n, lo_bit, shift, flag, s);
+        if (e != hipSuccess) return e;
+        uint32_t f = 0;
+        if ((e = hipMemcpyAsync(&f, flag, 4, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
+        if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
+        if (!f) return hipSuccess;   // (else: skewed buckets -- the segmented sort below redoes all)
     }
     size_t need = 0;
     e = rocprim::segmented_radix_sort_keys(nullptr, need, tmp, out, (unsigned)n, nbk, offs, offs + 1,

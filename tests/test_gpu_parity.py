@@ -504,3 +504,49 @@ def test_bucket_sort_skewed_keys(gpu, monkeypatch):
     e_o, f_o = O.boundary_features(lab, bnd)
     np.testing.assert_array_equal(out['edges'], e_o)
     check_features(out['features'], f_o)
+
+
+@pytest.mark.parametrize('packed', ['1', '0'])
+@pytest.mark.parametrize('shape,cell', [((48, 96, 130), 5), ((64, 128, 128), 3)])
+def test_lds_bucket_sort_matches_segmented(gpu, monkeypatch, packed, shape, cell):
+    """The in-LDS bucket sort (ctg_sort.hip k_bucket_lds_sort: one workgroup
+    per MSD bucket, sub-buckets above the LDS capacity) against rocPRIM's
+    segmented sort of the same buckets (CTG_LDS_SORT=0), on packed record keys
+    and on (key, slot) pairs (CTG_SORT_PACKED=0): same edges, counts, min /
+    max, features to the last bits of the record summation order -- and the
+    oracle."""
+    lab, bnd = S.generate(shape, cell=cell, seed=11)
+    monkeypatch.setenv('CTG_SORT_PACKED', packed)
+    monkeypatch.setenv('CTG_BUCKET_SORT_PAIRS', '1')
+    monkeypatch.setenv('CTG_LDS_SORT', '1')
+    out = rag.rag_features(lab, bnd)
+    monkeypatch.setenv('CTG_LDS_SORT', '0')
+    ref = rag.rag_features(lab, bnd)
+    np.testing.assert_array_equal(out['edges'], ref['edges'])
+    np.testing.assert_array_equal(out['nodes'], ref['nodes'])
+    np.testing.assert_array_equal(out['features'][:, [2, 8, 9]], ref['features'][:, [2, 8, 9]])
+    np.testing.assert_allclose(out['features'], ref['features'], rtol=1e-12, atol=1e-15)
+    e_o, f_o = O.boundary_features(lab, bnd)
+    np.testing.assert_array_equal(out['edges'], e_o)
+    check_features(out['features'], f_o)
+
+
+def test_lds_bucket_sort_skew_falls_back(gpu, monkeypatch):
+    """One edge with more records than a workgroup sorts in LDS: two planes
+    of two labels over 4096 x 4096 (one (1, 2) record per 64 x 32 tile, 8192
+    of them in one bucket).  The in-LDS sort flags the bucket and the
+    segmented sort redoes the pass: one edge, every face counted."""
+    lab = np.ones((2, 4096, 4096), np.uint64)
+    lab[1] = 2
+    bnd = np.zeros(lab.shape, np.float32)
+    bnd[0] = 0.25
+    bnd[1] = 0.75
+    monkeypatch.setenv('CTG_LDS_SORT', '1')
+    for packed in ('1', '0'):
+        monkeypatch.setenv('CTG_SORT_PACKED', packed)
+        monkeypatch.setenv('CTG_BUCKET_SORT_PAIRS', '1')
+        out = rag.rag_features(lab, bnd)
+        assert out['edges'].tolist() == [[1, 2]]
+        f = out['features'][0]
+        assert f[9] == 2 * 4096 * 4096 and f[0] == 0.5 and f[2] == 0.25 and f[8] == 0.75
+        assert abs(f[1] - 0.0625) < 1e-12
