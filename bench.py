@@ -53,7 +53,9 @@ WORKLOADS = {
     '1': (512, 10, None, 'weak', 'BASELINE configs[1]: %d^3 per GPU, cell %d, boundary map'),
     '2': (2048, 16, None, 'strong', 'BASELINE configs[2]: %d^3 boundary map, cell %d, z-slab sharded'),
     '3': (1024, 10, 'nn', 'strong', 'BASELINE configs[3]: %d^3, cell %d, 3-channel nearest-neighbour affinities'),
-    '3lr': (1024, 10, 'lr', 'strong', 'BASELINE configs[3]: %d^3, cell %d, 12-channel long-range affinities'),
+    '3lr': (1024, 10, 'lr', 'strong', 'BASELINE configs[3]: %d^3, cell %d, 12-channel long-range affinities '
+                                      '(whole-volume rule: a sample counts when its pair is an edge of the global '
+                                      'RAG; the per-block drop-in applies the block sub-graph rule, DESIGN 3.3)'),
     '4': (1024, 5, None, 'strong', 'BASELINE configs[4]: %d^3 high fragmentation, cell %d, boundary map'),
 }
 

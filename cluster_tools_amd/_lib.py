@@ -100,6 +100,7 @@ PROTOTYPES = {
                                           ctypes.c_int, c_vp, c_vp, ctypes.c_int]),
     'ctg_io_free': (None, [c_vp]),
     'ctg_io_cache_clear': (None, []),
+    'ctg_io_cache_stats': (None, [ctypes.c_void_p]),
     'ctg_io_cache_drop': (None, [ctypes.c_char_p]),
     'ctg_io_write_chunks': (ctypes.c_int, [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                            ctypes.c_int64, c_vp, c_vp, c_vp, c_vp, ctypes.c_int, ctypes.c_int,

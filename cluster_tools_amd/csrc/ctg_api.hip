@@ -1026,20 +1026,21 @@ int ctg_rag_features(const void* labels, int label_bits, const void* data, int d
             CTG_CHECK(hipStreamSynchronize(s));
         }
         if ((mx >> 32) == 0) {
-            // Bloom prefilter, 16 bits per edge: one load per long-range sample
-            // (vs. a probe chain in a set 4x the size); the reduce drops its
-            // false positives (keys no nearest-neighbour sample flagged)
+            // Bloom prefilter, 16 bits per stored direction (32 per edge): one
+            // load per long-range sample (vs. a probe chain in a set 4x the
+            // size); the reduce drops its false positives (keys no
+            // nearest-neighbour sample flagged)
             const char* bpk = getenv("CTG_BLOOM_BPK");   // A/B: bits per edge
-            const int64_t bits = adj_graph->n_edges * (bpk ? std::max(1, atoi(bpk)) : 16);
-            uint32_t words = 1024;
-            while ((int64_t)words * 64 < bits) words *= 2;
-            bloom = (unsigned long long*)dalloc((size_t)words * 8);
+            const int64_t bits = adj_graph->n_edges * (bpk ? std::max(1, atoi(bpk)) : 32);
+            uint32_t blocks = 128;   // 64-B blocks
+            while ((int64_t)blocks * 512 < bits) blocks *= 2;
+            bloom = (unsigned long long*)dalloc((size_t)blocks * 64);
             if (!bloom) {
                 ctg_free(adj_graph);
                 set_error("ctg_rag_features: out of memory (adjacency filter)");
                 return CTG_ERR_NOMEM;
             }
-            hipError_t e = launch_build_bloom(adj_graph->edges, adj_graph->n_edges, bloom, words - 1, s);
+            hipError_t e = launch_build_bloom(adj_graph->edges, adj_graph->n_edges, bloom, blocks - 1, s);
             if (e != hipSuccess) {
                 dfree(bloom);
                 ctg_free(adj_graph);
@@ -1047,7 +1048,7 @@ int ctg_rag_features(const void* labels, int label_bits, const void* data, int d
                 return CTG_ERR_HIP;
             }
             P.bloom = bloom;
-            P.bloom_mask = words - 1;
+            P.bloom_mask = blocks - 1;
         }
     }
     {

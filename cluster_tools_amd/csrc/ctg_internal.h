@@ -81,8 +81,13 @@ __host__ __device__ inline uint32_t hash_key(uint64_t k) {
     return (uint32_t)k;
 }
 
-// Blocked Bloom filter of RAG edge keys (the long-range affinity prefilter):
-// a key sets / tests 4 bits of ONE 64-bit word, so a query is a single load.
+// Blocked Bloom filter of RAG edge keys (the long-range affinity prefilter),
+// blocked by OWNER label: an edge (u, v) is stored twice, as u -> v in the
+// 64-B block of u and as v -> u in the block of v; a probe from a voxel of
+// label a for partner b tests a -> b: 4 bits of ONE 64-bit word of a's block.
+// A wave's probes then touch one cache line per distinct own label (a few per
+// row) instead of one per distinct pair, and the line of a label stays hot in
+// L2 over every channel and plane that label's cell spans.
 __host__ __device__ inline uint64_t bloom_hash(uint64_t k) {
     k ^= k >> 33;
     k *= 0xff51afd7ed558ccdull;
@@ -90,10 +95,15 @@ __host__ __device__ inline uint64_t bloom_hash(uint64_t k) {
     k *= 0xc4ceb9fe1a85ec53ull;
     return k ^ (k >> 32);
 }
+// h: bloom_hash((owner << 32) | other)
 __host__ __device__ inline uint64_t bloom_bits(uint64_t h) {
     return (1ull << (h & 63)) | (1ull << ((h >> 6) & 63)) | (1ull << ((h >> 12) & 63)) | (1ull << ((h >> 18) & 63));
 }
-__host__ __device__ inline uint32_t bloom_word(uint64_t h, uint32_t mask) { return (uint32_t)(h >> 40) & mask; }
+// word of the owner's block (block_mask = blocks - 1, 8 words per block)
+__host__ __device__ inline uint32_t bloom_block(uint32_t owner, uint32_t block_mask) {
+    return ((uint32_t)(bloom_hash(owner) >> 24) & block_mask) * 8u;
+}
+__host__ __device__ inline uint32_t bloom_word(uint32_t block, uint64_t h) { return block + ((uint32_t)(h >> 40) & 7u); }
 
 // ---------------------------------------------------------------------------
 // records: the face scan flushes one record per (tile, edge)
@@ -145,7 +155,7 @@ struct ScanParams {
     int ablate;                // diagnostic: 8 loads only, 32 staging without fold
     // long-range affinity channels: samples whose (u,v) fails this blocked
     // Bloom filter of the RAG edge keys ((u << 32) | v) are dropped in the scan
-    // (bloom_mask = words - 1); the reduce drops the false positives, keeping
+    // (bloom_mask = blocks - 1, 8 words a block); the reduce drops the false positives, keeping
     // only keys that nearest-neighbour samples (MARK_ONE_ADJ) flagged
     const unsigned long long* bloom;
     uint32_t bloom_mask;

@@ -30,6 +30,7 @@
 #include <list>
 #include <memory>
 #include <mutex>
+#include <sstream>
 #include <string>
 #include <sys/stat.h>
 #include <thread>
@@ -413,6 +414,11 @@ ChunkPtr decode_chunk(const std::string& path, int format, int ndim, const int64
     return c;
 }
 
+// cache statistics (ctg_io_cache_stats): reads served by the cache (ready or
+// in flight), decodes on a caller's thread, decodes on the readahead pool
+std::atomic<int64_t> g_stat_hits{0}, g_stat_decodes{0}, g_stat_prefetched{0};
+thread_local bool t_prefetch_thread = false;
+
 ChunkPtr get_chunk(const std::string& path, int format, int ndim, const int64_t* chunks, int es, bool swap,
                    int compression, bool* missing, std::string* err) {
     const size_t budget = cache_budget();
@@ -435,6 +441,7 @@ ChunkPtr get_chunk(const std::string& path, int format, int ndim, const int64_t*
                 wait_for = e.fut;
             } else if (e.stamp == st) {
                 g_lru.splice(g_lru.begin(), g_lru, e.lru);
+                if (!t_prefetch_thread) ++g_stat_hits;
                 return e.fut.get();
             } else {   // the file changed: decode again
                 g_cache_bytes -= e.bytes;
@@ -451,9 +458,13 @@ ChunkPtr get_chunk(const std::string& path, int format, int ndim, const int64_t*
     }
     if (wait_for.valid()) {
         ChunkPtr c = wait_for.get();
-        if (c) return c;
+        if (c) {
+            if (!t_prefetch_thread) ++g_stat_hits;
+            return c;
+        }
         return decode_chunk(path, format, ndim, chunks, es, swap, compression, missing, err);
     }
+    ++(t_prefetch_thread ? g_stat_prefetched : g_stat_decodes);
     ChunkPtr c = decode_chunk(path, format, ndim, chunks, es, swap, compression, missing, err);
     prom.set_value(c);
     std::lock_guard<std::mutex> g(g_cache_mu);
@@ -482,12 +493,17 @@ ChunkPtr get_chunk(const std::string& path, int format, int ndim, const int64_t*
 }
 
 // ---------------------------------------------------------------------------
-// Readahead: a job that walks its blocks in C order (one per call: the
-// reference's per-block API, initial_sub_graphs.py:146-157) decodes each
-// block's chunks only when its call arrives, a few chunks at a time.  After
-// every box read, the chunk box that follows it in C order (same extent) is
-// queued for decode into the cache on a small background pool, so the next
-// call finds its chunks inflated.  CTG_IO_READAHEAD=0 disables it.
+// Readahead: a job that walks its blocks one per call (the reference's
+// per-block API, initial_sub_graphs.py:146-157) decodes each block's chunks
+// only when its call arrives, a few chunks at a time.  After every box read,
+// the box this caller most likely reads next is queued for decode into the
+// cache on a small background pool, so the next call finds its chunks
+// inflated.  The guess follows the caller's own stride: a job of n_jobs walks
+// every n_jobs-th block (block_list[k::n_jobs], cluster_tasks.py), so the box
+// one stride past this one -- the stride being the step between this thread's
+// last two reads of the dataset -- and the next box in C order before a
+// stride is known.  A guess outside the chunk grid (the stride wrapping to the
+// next row) queues nothing.  CTG_IO_READAHEAD=0 disables it.
 // ---------------------------------------------------------------------------
 class Prefetcher {
 public:
@@ -519,6 +535,7 @@ private:
     static constexpr int kThreads = 8;
     static constexpr size_t kMaxQueued = 64;
     void run() {
+        t_prefetch_thread = true;
         while (true) {
             std::function<void()> f;
             {
@@ -544,6 +561,48 @@ bool readahead_on() {
         return !(e && e[0] == '0');
     }();
     return on && cache_budget() > 0;
+}
+
+// (dataset, thread) -> the chunk origin of that thread's previous box read
+struct LastBox {
+    int ndim;
+    int64_t c0[MAXD];
+};
+std::mutex& last_box_mu() {
+    static std::mutex* m = new std::mutex;   // never destroyed (see g_cache)
+    return *m;
+}
+std::unordered_map<std::string, LastBox>& last_box() {
+    static auto* m = new std::unordered_map<std::string, LastBox>;
+    return *m;
+}
+
+// the origin of the box to queue after a read at c0: c0 + (c0 - previous c0)
+// once this thread has read the dataset before with a nonzero step, else
+// false (the caller falls back to the C-order successor); records c0
+bool strided_next_box(const char* ds_path, int ndim, const int64_t* grid, const int64_t* c0, int64_t* nxt) {
+    std::ostringstream key;
+    key << ds_path << '#' << std::this_thread::get_id();
+    std::lock_guard<std::mutex> g(last_box_mu());
+    auto& m = last_box();
+    auto it = m.find(key.str());
+    bool have = false;
+    if (it != m.end() && it->second.ndim == ndim) {
+        bool nonzero = false, inside = true;
+        for (int a = 0; a < ndim; ++a) {
+            const int64_t d = c0[a] - it->second.c0[a];
+            nonzero = nonzero || d != 0;
+            nxt[a] = c0[a] + d;
+            inside = inside && nxt[a] >= 0 && nxt[a] < grid[a];
+        }
+        have = nonzero;
+        if (have && !inside) nxt[0] = -1;   // a known stride that leaves the grid: queue nothing
+    }
+    if (m.size() > 4096) m.clear();   // bounded: one entry per (dataset, thread) in practice
+    LastBox& lb = m[key.str()];
+    lb.ndim = ndim;
+    std::copy(c0, c0 + ndim, lb.c0);
+    return have;
 }
 
 // chunk box [c0, c0 + nc) -> the box after it in C order (last axis first;
@@ -667,7 +726,8 @@ int ctg_io_read_box(const char* ds_path, int format, int dtype_size, int big_end
             nxt[a] = c0[a];
             cnt[a] = nc[a];
         }
-        if (next_chunk_box(ndim, grid, nxt, cnt)) {
+        const bool strided = strided_next_box(ds_path, ndim, grid, c0, nxt);
+        if (strided ? nxt[0] >= 0 : next_chunk_box(ndim, grid, nxt, cnt)) {
             const std::string ds(ds_path);
             std::vector<int64_t> ch(chunks, chunks + ndim);
             for (int64_t ci = 0; ci < n_chunks; ++ci) {
@@ -766,6 +826,13 @@ void ctg_io_free(void* p) { free(p); }
 
 void ctg_io_cache_drop(const char* chunk_path) {
     if (chunk_path) cache_drop(chunk_path);
+}
+
+void ctg_io_cache_stats(int64_t* out) {
+    if (!out) return;
+    out[0] = g_stat_hits.load();
+    out[1] = g_stat_decodes.load();
+    out[2] = g_stat_prefetched.load();
 }
 
 void ctg_io_cache_clear(void) {

@@ -327,20 +327,25 @@ __global__ void k_u32_to_u64(int64_t n, const uint32_t* __restrict__ in, uint64_
     if (i < n) out[i] = in[i];
 }
 
-// blocked Bloom filter of the RAG edge keys (u << 32) | v (labels < 2^32), the
-// long-range affinity prefilter of the face scan
-__global__ void k_build_bloom(const uint64_t* __restrict__ edges, int64_t E, unsigned long long* words, uint32_t mask) {
+// owner-blocked Bloom filter of the RAG edges (labels < 2^32; ctg_internal.h):
+// u -> v into u's block and v -> u into v's block, the long-range affinity
+// prefilter of the face scan
+__global__ void k_build_bloom(const uint64_t* __restrict__ edges, int64_t E, unsigned long long* words,
+                              uint32_t block_mask) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= E) return;
-    const uint64_t h = bloom_hash((edges[2 * i] << 32) | edges[2 * i + 1]);
-    atomicOr(&words[bloom_word(h, mask)], (unsigned long long)bloom_bits(h));
+    const uint32_t u = (uint32_t)edges[2 * i], v = (uint32_t)edges[2 * i + 1];
+    const uint64_t hu = bloom_hash(((uint64_t)u << 32) | v), hv = bloom_hash(((uint64_t)v << 32) | u);
+    atomicOr(&words[bloom_word(bloom_block(u, block_mask), hu)], (unsigned long long)bloom_bits(hu));
+    atomicOr(&words[bloom_word(bloom_block(v, block_mask), hv)], (unsigned long long)bloom_bits(hv));
 }
 
-hipError_t launch_build_bloom(const uint64_t* edges, int64_t E, unsigned long long* words, uint32_t mask,
+hipError_t launch_build_bloom(const uint64_t* edges, int64_t E, unsigned long long* words, uint32_t block_mask,
                               hipStream_t s) {
-    hipError_t e = hipMemsetAsync(words, 0, ((size_t)mask + 1) * 8, s);
+    hipError_t e = hipMemsetAsync(words, 0, ((size_t)block_mask + 1) * 64, s);
     if (e != hipSuccess || E == 0) return e;
-    hipLaunchKernelGGL(k_build_bloom, dim3((unsigned)((E + 255) / 256)), dim3(256), 0, s, edges, E, words, mask);
+    hipLaunchKernelGGL(k_build_bloom, dim3((unsigned)((E + 255) / 256)), dim3(256), 0, s, edges, E, words,
+                       block_mask);
     return hipGetLastError();
 }
 

@@ -982,11 +982,13 @@ __global__ __launch_bounds__(SCAN_THREADS, CTG_SCAN_MIN_WAVES) void k_face_scan(
                         if (glr && P.bloom != nullptr && !(ablate & 512)) {
                             uint64_t hb[K];
                             unsigned long long wb[K];
+                            uint32_t blk[ROWS];   // the own label's block (owner-blocked filter)
+#pragma unroll
+                            for (int r = 0; r < ROWS; ++r) blk[r] = bloom_block(Lc[r], P.bloom_mask);
 #pragma unroll
                             for (int k = 0; k < K; ++k) {
-                                const uint32_t lc = Lc[k % ROWS];
-                                hb[k] = bloom_hash(((uint64_t)min(lc, lq[k]) << 32) | max(lc, lq[k]));
-                                wb[k] = (act[k] && (glr >> (k / ROWS) & 1u)) ? P.bloom[bloom_word(hb[k], P.bloom_mask)]
+                                hb[k] = bloom_hash(((uint64_t)Lc[k % ROWS] << 32) | lq[k]);
+                                wb[k] = (act[k] && (glr >> (k / ROWS) & 1u)) ? P.bloom[bloom_word(blk[k % ROWS], hb[k])]
                                                                              : ~0ull;
                             }
 #pragma unroll

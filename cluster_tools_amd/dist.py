@@ -140,16 +140,44 @@ def segment_words(counts_all, world, rank):
 
 
 class DistResult:
-    """This rank's shard of the global (sorted) edge table + features + nodes."""
+    """This rank's shard of the global (sorted) edge table + features + nodes.
 
-    def __init__(self, shard, edge_offset, n_edges_global, node_offset, n_nodes_global, info, sizes):
+    The shard sizes of every rank are all-gathered on the stream when the call
+    returns; the host reads them (one read, ``_host(..., 'offsets')``) only when
+    an offset, a global count or ``shard_sizes`` is first asked for, so a
+    caller that works on its shard alone never waits for them."""
+
+    def __init__(self, shard, sizes_all, rank, info):
         self.shard = shard            # rag.Result (HIP) or the test backend's shard
-        self.edge_offset = edge_offset
-        self.n_edges_global = n_edges_global
-        self.node_offset = node_offset
-        self.n_nodes_global = n_nodes_global
-        self.shard_sizes = sizes      # [(edges, nodes)] of every rank
+        self._sizes_all = sizes_all   # (world*2,) int64 tensor: (edges, nodes) of every rank
+        self._rank = rank
+        self._sizes = None
         self._info = info
+
+    @property
+    def shard_sizes(self):
+        """[(edges, nodes)] of every rank."""
+        if self._sizes is None:
+            a = _host(self._sizes_all, 'offsets').reshape(-1, 2).tolist()
+            self._sizes = [tuple(int(v) for v in row) for row in a]
+            self._sizes_all = None
+        return self._sizes
+
+    @property
+    def edge_offset(self):
+        return sum(s[0] for s in self.shard_sizes[:self._rank])
+
+    @property
+    def n_edges_global(self):
+        return sum(s[0] for s in self.shard_sizes)
+
+    @property
+    def node_offset(self):
+        return sum(s[1] for s in self.shard_sizes[:self._rank])
+
+    @property
+    def n_nodes_global(self):
+        return sum(s[1] for s in self.shard_sizes)
 
     @property
     def n_edges(self):
@@ -179,16 +207,6 @@ class DistResult:
 
     def free(self):
         self.shard.free()
-
-
-def _exclusive_offsets(n_locals, group, device):
-    """[(offset of this rank, total)] for each local count, one all_gather;
-    and every rank's counts."""
-    t = torch.tensor(list(n_locals), dtype=torch.int64, device=_wire_device(device, group))
-    allc = _host(all_gather_flat(t, group), 'offsets').reshape(-1, len(n_locals)).tolist()
-    r = dist.get_rank(group)
-    return ([(sum(row[k] for row in allc[:r]), sum(row[k] for row in allc)) for k in range(len(n_locals))],
-            [tuple(row) for row in allc])
 
 
 def slab_plan(Z, world, rank, offsets=None):
@@ -282,9 +300,12 @@ def rag_features_distributed(labels, data=None, offsets=None, own_begin=None, ow
         phase('merge')
     finally:
         loc.free()
-    (e_off_tot, n_off_tot), sizes = _exclusive_offsets([shard.n_edges, shard.n_nodes], group, dev)
+    # the global offsets: every rank's shard sizes, gathered now (collective
+    # order), read by the host on first use (DistResult)
+    sizes = all_gather_flat(torch.tensor([int(shard.n_edges), int(shard.n_nodes)], dtype=torch.int64,
+                                         device=wire), group)
     phase('offsets')
-    return DistResult(shard, e_off_tot[0], e_off_tot[1], n_off_tot[0], n_off_tot[1], info, sizes)
+    return DistResult(shard, sizes, rank, info)
 
 
 def _any_exchange(counts_all, world):

@@ -291,6 +291,10 @@ void ctg_io_free(void* p);
  * default 4096; an entry is reused only while its file keeps its inode, size,
  * mtime and ctime -- every writer here replaces chunk files by rename) */
 void ctg_io_cache_clear(void);
+/* cache counters since process start: out[0] chunk reads the cache served
+ * (decoded, or in flight on the readahead pool), out[1] decodes on the
+ * caller's threads, out[2] decodes by the readahead pool */
+void ctg_io_cache_stats(int64_t* out);
 /* drop the cached decodes of one chunk file (writers outside ctg_io call it) */
 void ctg_io_cache_drop(const char* chunk_path);
 /* write n_chunks chunks (default mode with chunk_shapes, or N5 varlength) */

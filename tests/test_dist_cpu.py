@@ -212,7 +212,9 @@ def _reads_worker(rank, world, port, outdir):
         del cdist.host_reads[:]
         res = cdist.rag_features_distributed(np.ascontiguousarray(lab[rd:end]), np.ascontiguousarray(bnd[rd:end]),
                                              own_begin=(own - rd, 0, 0), backend=OracleBackend())
-        reads.append('|'.join(cdist.host_reads))
+        reads.append('|'.join(cdist.host_reads))   # the call itself: the count matrix only
+        _ = (res.edge_offset, res.n_edges_global, res.node_offset, res.shard_sizes)
+        reads.append('|'.join(cdist.host_reads))   # the shard sizes, once, on first use
         np.save(os.path.join(outdir, 'e%d_%d.npy' % (Z, rank)), res.edges())
         np.save(os.path.join(outdir, 'f%d_%d.npy' % (Z, rank)), res.features())
     np.save(os.path.join(outdir, 'reads%d.npy' % rank), np.array(reads))
@@ -222,8 +224,8 @@ def _reads_worker(rank, world, port, outdir):
 def test_changing_slab_shapes_and_host_reads(tmp_path):
     """No state is carried between calls (a capacity plan cached
     per slab shape could disagree between ranks): Z = 100 then Z = 101 over 3
-    ranks both equal the whole-volume oracle, and every call reads exactly the
-    count matrix and the shard sizes on the host."""
+    ranks both equal the whole-volume oracle; every call reads exactly the
+    count matrix on the host, and the shard sizes once when first used."""
     world = 3
     mp.spawn(_reads_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
     for Z in (100, 101):
@@ -234,7 +236,7 @@ def test_changing_slab_shapes_and_host_reads(tmp_path):
         np.testing.assert_array_equal(e, e_ref)
         np.testing.assert_allclose(f, f_ref, rtol=1e-9, atol=1e-12)
     for r in range(world):
-        assert list(np.load(tmp_path / ('reads%d.npy' % r))) == ['counts|offsets'] * 2
+        assert list(np.load(tmp_path / ('reads%d.npy' % r))) == ['counts', 'counts|offsets'] * 2
 
 
 def test_mgpu_slab_plan_c_abi():

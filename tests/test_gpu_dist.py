@@ -94,7 +94,9 @@ def _rccl_worker(rank, world, port, outdir, affinity):
     np.save(os.path.join(outdir, 'e.npy'), res.edges())
     np.save(os.path.join(outdir, 'f.npy'), res.features())
     np.save(os.path.join(outdir, 'n.npy'), res.node_shard.cpu().numpy())
-    np.save(os.path.join(outdir, 'reads.npy'), np.array(list(cdist.host_reads)))
+    calls_reads = list(cdist.host_reads)
+    assert res.edge_offset == 0 and res.n_edges_global == res.n_edges   # the lazy shard-size read
+    np.save(os.path.join(outdir, 'reads.npy'), np.array(calls_reads + list(cdist.host_reads)))
     dist.destroy_process_group()
 
 
@@ -111,8 +113,8 @@ def test_rccl_world1_exchange_equals_single_call(tmp_path, affinity):
     np.testing.assert_array_equal(np.load(tmp_path / 'e.npy'), ref['edges'])
     np.testing.assert_allclose(np.load(tmp_path / 'f.npy'), ref['features'], rtol=1e-9, atol=1e-12)
     np.testing.assert_array_equal(np.load(tmp_path / 'n.npy').astype(np.uint64), ref['nodes'])
-    # one count-matrix read and one shard-size read per call
-    assert list(np.load(tmp_path / 'reads.npy')) == ['counts', 'offsets']
+    # one count-matrix read per call; the shard sizes when first asked for
+    assert list(np.load(tmp_path / 'reads.npy')) == ['counts', 'counts', 'offsets']
 
 
 @pytest.mark.parametrize('affinity', [False, True])

@@ -384,6 +384,55 @@ def test_native_chunk_cache_sees_rewrites_and_threads(tmp_path, monkeypatch):
     n5._native().ctg_io_cache_clear()
 
 
+def test_native_readahead_follows_the_job_stride(tmp_path, monkeypatch):
+    """ADVICE r3 (low): a job walks every n_jobs-th block (block_list[k::n_jobs]),
+    so the readahead queues the box one stride past the last read (the step
+    between this thread's last two reads of the dataset), not the C-order
+    successor, which belongs to another job."""
+    import ctypes
+    import time
+    _with_codec(monkeypatch, True)
+    lib = n5._native()
+    p = str(tmp_path / 's.n5')
+    data = np.arange(8 * 16 * 16 * 12, dtype=np.uint64).reshape(8, 16, 16 * 12)
+    with n5.File(p) as f:
+        ds = f.create_dataset('d', shape=data.shape, chunks=(8, 16, 16), dtype='uint64', compression='gzip')
+        ds[:] = data
+        lib.ctg_io_cache_clear()
+
+        def stats():
+            out = np.zeros(3, np.int64)
+            lib.ctg_io_cache_stats(out.ctypes.data_as(ctypes.c_void_p))
+            return out
+
+        def settle(before):
+            for _ in range(200):   # the readahead pool works in the background
+                s = stats()
+                if s[2] > before[2]:
+                    return s
+                time.sleep(0.01)
+            return stats()
+
+        def read(i):
+            np.testing.assert_array_equal(ds[:, :, 16 * i:16 * i + 16], data[:, :, 16 * i:16 * i + 16])
+
+        s0 = stats()
+        read(0)                  # no history: the C-order successor (block 1) is queued
+        s1 = settle(s0)
+        assert s1[1] - s0[1] == 1 and s1[2] - s0[2] == 1
+        read(3)                  # stride 3: block 6 is queued
+        s2 = settle(s1)
+        assert s2[1] - s1[1] == 1 and s2[2] - s1[2] == 1
+        read(6)                  # served by the readahead; block 9 queued next
+        s3 = settle(s2)
+        assert s3[0] - s2[0] == 1 and s3[1] == s2[1] and s3[2] - s2[2] == 1
+        read(9)                  # hit again; the next guess (12) leaves the grid: nothing queued
+        time.sleep(0.1)
+        s4 = stats()
+        assert s4[0] - s3[0] == 1 and s4[1] == s3[1] and s4[2] == s3[2]
+    lib.ctg_io_cache_clear()
+
+
 def test_native_writer_follows_the_declared_stream_type(tmp_path, monkeypatch):
     """N5 gzip with "useZlib": true and zarr "zlib" get zlib streams from the
     native writer (plain zlib.decompress reads them), N5 / zarr "gzip" get gzip

@@ -1,7 +1,8 @@
 """Run the hot path a few times on a resident synthetic volume (for rocprofv3).
 
 usage: prof_scan.py [boundary|graph|nn|lr]   (CTG_PROF_SIZE, CTG_PROF_CELL,
-CTG_PROF_ITERS select the cube edge, cell size and repetitions)."""
+CTG_PROF_ITERS select the cube edge, cell size and repetitions;
+CTG_PROF_CHANNELS="0,1,2,..." a subset of the affinity channels)."""
 import os
 import sys
 
@@ -18,6 +19,10 @@ if mode in ('nn', 'lr'):
     offsets = synthetic.NN_OFFSETS if mode == 'nn' else synthetic.LR_OFFSETS
     data = rag.synth_affinities(bnd, offsets)
     del bnd
+    if os.environ.get('CTG_PROF_CHANNELS'):
+        idx = [int(c) for c in os.environ['CTG_PROF_CHANNELS'].split(',')]
+        data, offsets = data[idx].contiguous(), [offsets[i] for i in idx]
+        torch.cuda.empty_cache()
 elif mode == 'graph':
     data = None
 torch.cuda.synchronize()
