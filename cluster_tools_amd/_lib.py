@@ -135,6 +135,8 @@ def load():
                 "or `make -C cluster_tools_amd/csrc` (the HIP path has no CPU fallback)" % LIB_PATH)
         lib = ctypes.CDLL(LIB_PATH)
         for name, (res, args) in PROTOTYPES.items():
+            if os.environ.get('CTG_LIB') and not hasattr(lib, name):
+                continue   # an older A/B build (tools/ab_variants.py) without a newer entry point
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args
