@@ -959,6 +959,9 @@ int ctg_rag_features(const void* labels, int label_bits, const void* data, int d
     // depend on it: ctg_scan.hip's per-wave sample budget bounds every count)
     P.check_planes = 8;
     if (const char* cp = getenv("CTG_CHECK_PLANES")) P.check_planes = std::max(1, atoi(cp));
+    // planes per workgroup of the narrow-tile launch (fragmented volumes):
+    // shallower tiles split fewer edges at table flushes (profiles/r4/tz)
+    constexpr int NARROW_TILE_Z = 16;
     // planes per workgroup: 32, fewer where that leaves < ~1024 workgroups,
     // 64 (128) where even 64 (128)-plane tiles give >= 32 K workgroups (A/B with the 5/8
     // table fill, 32 vs 64 planes: 512^3 step 1.027 -> 1.014 ms, configs[4]
@@ -973,7 +976,9 @@ int ctg_rag_features(const void* labels, int label_bits, const void* data, int d
         // profiles/r4/ablate)
         if (cols * ((shape[0] + 127) / 128) >= 32768) tz = 128;
         while (tz > 8 && cols * ((shape[0] + tz - 1) / tz) < 1024) tz /= 2;
-        if (const char* t = getenv("CTG_TILE_Z")) tz = std::max(1, atoi(t));
+        P.tile_z_narrow = std::min(tz, NARROW_TILE_Z);
+        if (const char* t = getenv("CTG_TILE_Z")) P.tile_z_narrow = tz = std::max(1, atoi(t));
+        if (const char* t = getenv("CTG_TILE_Z_NARROW")) P.tile_z_narrow = std::max(1, atoi(t));
         P.tile_z = tz;
     }
     {
@@ -1026,12 +1031,13 @@ int ctg_rag_features(const void* labels, int label_bits, const void* data, int d
             CTG_CHECK(hipStreamSynchronize(s));
         }
         if ((mx >> 32) == 0) {
-            // Bloom prefilter, 16 bits per stored direction (32 per edge): one
+            // Bloom prefilter, 24 bits per stored direction (48 per edge; 32: +3 %
+            // records, 12-channel scan +0.5 ms, profiles/r4/tz): one
             // load per long-range sample (vs. a probe chain in a set 4x the
             // size); the reduce drops its false positives (keys no
             // nearest-neighbour sample flagged)
             const char* bpk = getenv("CTG_BLOOM_BPK");   // A/B: bits per edge
-            const int64_t bits = adj_graph->n_edges * (bpk ? std::max(1, atoi(bpk)) : 32);
+            const int64_t bits = adj_graph->n_edges * (bpk ? std::max(1, atoi(bpk)) : 48);
             uint32_t blocks = 128;   // 64-B blocks
             while ((int64_t)blocks * 512 < bits) blocks *= 2;
             bloom = (unsigned long long*)dalloc((size_t)blocks * 64);

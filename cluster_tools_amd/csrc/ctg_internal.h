@@ -150,6 +150,7 @@ struct ScanParams {
     double scale, offset;      // histogram mapping
     double u8_scale;           // uint8 -> float factor (1/255)
     int tile_z;                // z-planes per workgroup
+    int tile_z_narrow;         // z-planes per workgroup of the narrow-tile launch (0: tile_z)
     int check_planes;          // planes between flush decisions
     int fast40;                // histogram range [0,1) x 40 bins: exact f32 binning
     int ablate;                // diagnostic: 8 loads only, 32 staging without fold

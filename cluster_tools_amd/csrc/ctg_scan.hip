@@ -1098,9 +1098,10 @@ static hipError_t launch_scan_r(const ScanParams& P, const RecordBuf& R, Counter
     ScanParams Q = P;
     int64_t nwg = P.batch_tiles;
     if (!P.blocks) {
+        if (NR == ROWS_NARROW && ROWS_NARROW != ROWS_WIDE && P.tile_z_narrow > 0) Q.tile_z = P.tile_z_narrow;
         Q.ntiles[0] = (P.shape[2] + TILE_X - 1) / TILE_X;
         Q.ntiles[1] = (P.shape[1] + NR * WAVES - 1) / (NR * WAVES);
-        Q.ntiles[2] = (P.shape[0] + P.tile_z - 1) / P.tile_z;
+        Q.ntiles[2] = (P.shape[0] + Q.tile_z - 1) / Q.tile_z;
         nwg = Q.ntiles[0] * Q.ntiles[1] * Q.ntiles[2];
     }
     if (nwg <= 0) return hipSuccess;

@@ -1,7 +1,7 @@
 #!/bin/bash
 # One GPU call for a round's profile evidence (output: gpurun_out/$TAG/...):
 #  * rocprofv3 --kernel-trace --stats of every bench line: the default
-#    (configs[1]), configs[2] (2048^3), configs[3] (3-channel, 12-channel),
+#    (configs[2], 2048^3), configs[1], configs[3] (3-channel, 12-channel),
 #    configs[4], and the configs[0] batched per-block scan (tools/prof_blocks.py);
 #  * FETCH_SIZE and WRITE_SIZE passes (each its own rocprofv3 run, no tracing
 #    domain beside --pmc) of the face scan on the same workloads
@@ -42,7 +42,7 @@ for c in $CONFIGS; do
   else
     if [ "$c" = 1 ]; then
       timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace_c1 -o run -- \
-          python bench.py --steps 20 --warmup 3 --no-cpu-baseline > $O/bench_traced_c1.json 2> $O/trace_c1.err
+          python bench.py --config 1 --steps 20 --warmup 3 --no-cpu-baseline > $O/bench_traced_c1.json 2> $O/trace_c1.err
     else
       timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace_c$c -o run -- \
           python bench.py --config $c --steps 5 --warmup 1 --no-cpu-baseline > $O/bench_traced_c$c.json 2> $O/trace_c$c.err
