@@ -209,73 +209,6 @@ __global__ __launch_bounds__(256) void k_reduce_edges(int64_t E, const uint32_t*
     }
 }
 
-// The narrow-record reduce with the record bodies staged through LDS: a
-// workgroup's 256 edges own one contiguous range of sorted record positions
-// (offs[e0] .. offs[e_last] + runs[e_last]); it walks that range in chunks of
-// RL_CAP records, eight lanes per record load its 128-B body (16 B each: one
-// cache line per eight lanes, instead of one thread issuing eight 16-B loads
-// into eight different lines with every other lane of the wave), and each
-// thread then folds its own edge's records of the chunk from LDS, in sorted
-// order -- the same additions in the same order as k_reduce_edges.
-constexpr int RL_CAP = 256;                      // records per chunk
-constexpr int RL_PITCH = 9;                      // uint4 per staged record (8 + 1 pad: fewer bank conflicts)
-constexpr int RL_BATCH = 1;                      // loads in flight per lane
-
-__global__ __launch_bounds__(256) void k_reduce_edges_lds(int64_t E, const uint32_t* __restrict__ dE,
-                                                          const uint64_t* __restrict__ uniq,
-                                                          const uint32_t* __restrict__ runs,
-                                                          const uint32_t* __restrict__ offs, Perm perm,
-                                                          RecordBuf R, int nb, uint64_t umask, int need_adj,
-                                                          int ignore_label, double scale, double offset,
-                                                          ReduceOut O) {
-    __shared__ uint4 buf[RL_CAP * RL_PITCH];
-    const int64_t e0 = (int64_t)blockIdx.x * 256;
-    const int64_t e = e0 + threadIdx.x;
-    if (e == 0 && O.count_out) *O.count_out = *dE;
-    const int64_t Ed = min(E, (int64_t)*dE);
-    if (e0 >= Ed) return;   // uniform over the workgroup
-    const int64_t el = min(e0 + 255, Ed - 1);
-    const uint32_t rb = offs[e0], re = offs[el] + runs[el];
-    const bool act = e < Ed;
-    uint64_t u = 0;
-    uint32_t b = 0, n = 0;
-    if (act) {
-        const uint64_t sk = uniq[e];
-        u = sk >> nb;
-        O.edges[2 * e] = u;
-        O.edges[2 * e + 1] = sk & ((1ull << nb) - 1ull);
-        b = offs[e];
-        n = runs[e];
-    }
-    uint32_t h[NSLOTS];
-#pragma unroll
-    for (int j = 0; j < NSLOTS; ++j) h[j] = 0;
-    uint32_t cnt = 0, flags = 0, mn = ORD_POS_INF, mx = ORD_NEG_INF;
-    Moments mo;
-    for (uint32_t c0 = rb; c0 < re; c0 += RL_CAP) {
-        const uint32_t cn = min((uint32_t)RL_CAP, re - c0);
-        __syncthreads();   // the previous chunk is folded
-        for (uint32_t f0 = threadIdx.x; f0 < cn * 8; f0 += 256 * RL_BATCH) {
-            uint4 t[RL_BATCH];
-#pragma unroll
-            for (int k = 0; k < RL_BATCH; ++k) {
-                const uint32_t f = f0 + 256u * k;
-                if (f < cn * 8)
-                    t[k] = reinterpret_cast<const uint4*>(R.hist + (size_t)perm(c0 + (f >> 3)) * NREC_STRIDE)[f & 7];
-            }
-#pragma unroll
-            for (int k = 0; k < RL_BATCH; ++k) {
-                const uint32_t f = f0 + 256u * k;
-                if (f < cn * 8) buf[(f >> 3) * RL_PITCH + (f & 7)] = t[k];
-            }
-        }
-        __syncthreads();
-        const uint32_t lo = max(b, c0), hi = min(b + n, c0 + cn);
-        for (uint32_t r = lo; r < hi; ++r) add_narrow(&buf[(r - c0) * RL_PITCH], h, cnt, flags, mn, mx, mo);
-    }
-    if (act) reduce_epilogue(e, u, h, cnt, flags, mn, mx, mo, umask, need_adj, ignore_label, scale, offset, O);
-}
-
 // 16 threads per edge (one per 8-B feature / 16-B stats word): the copies of
 // consecutive kept rows are coalesced
 __global__ void k_compact(int64_t E, const uint32_t* __restrict__ dE, const uint32_t* __restrict__ keep,
@@ -631,15 +564,6 @@ hipError_t launch_max_pairs(int64_t n, const uint64_t* uv, unsigned long long* o
     hipLaunchKernelGGL(k_max_pairs, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, n, uv, out);
     return hipGetLastError();
 }
-// CTG_REDUCE_LDS=0: the one-thread-per-edge loads of k_reduce_edges (A/B)
-static bool reduce_lds() {
-    static const bool on = [] {
-        const char* e = getenv("CTG_REDUCE_LDS");
-        return !(e && e[0] == '0');
-    }();
-    return on;
-}
-
 hipError_t launch_reduce(int64_t E, const uint32_t* dE, const uint64_t* uniq, const uint32_t* runs,
                          const uint32_t* offs, const uint32_t* perm32, const uint64_t* perm64, int ib,
                          const RecordBuf& R, int wide, int stats, int nb, uint64_t umask, int need_adj,
@@ -651,10 +575,7 @@ hipError_t launch_reduce(int64_t E, const uint32_t* dE, const uint64_t* uniq, co
         if (stats) hipLaunchKernelGGL((k_reduce_edges<true, true>), g, b, 0, s, E, dE, uniq, runs, offs, perm, R, nb, umask, need_adj, ignore_label, scale, offset, O);
         else hipLaunchKernelGGL((k_reduce_edges<true, false>), g, b, 0, s, E, dE, uniq, runs, offs, perm, R, nb, umask, need_adj, ignore_label, scale, offset, O);
     } else {
-        if (stats && reduce_lds() && O.ablate == 0)
-            hipLaunchKernelGGL(k_reduce_edges_lds, g, b, 0, s, E, dE, uniq, runs, offs, perm, R, nb, umask, need_adj,
-                               ignore_label, scale, offset, O);
-        else if (stats) hipLaunchKernelGGL((k_reduce_edges<false, true>), g, b, 0, s, E, dE, uniq, runs, offs, perm, R, nb, umask, need_adj, ignore_label, scale, offset, O);
+        if (stats) hipLaunchKernelGGL((k_reduce_edges<false, true>), g, b, 0, s, E, dE, uniq, runs, offs, perm, R, nb, umask, need_adj, ignore_label, scale, offset, O);
         else hipLaunchKernelGGL((k_reduce_edges<false, false>), g, b, 0, s, E, dE, uniq, runs, offs, perm, R, nb, umask, need_adj, ignore_label, scale, offset, O);
     }
     return hipGetLastError();
