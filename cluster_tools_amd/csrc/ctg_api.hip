@@ -18,6 +18,7 @@
 namespace ctg {
 hipError_t launch_face_scan(const ScanParams& P, const RecordBuf& R, Counters* C, hipStream_t s);
 int scan_tile_rows();
+int scan_tile_rows_narrow();
 hipError_t launch_density(const void* L, int label_bits, const int64_t* shape, int n_rows, uint32_t* out,
                           hipStream_t s);
 hipError_t launch_unique_tiles(const uint64_t* L, const int64_t* shape, const int64_t* b, const int64_t* e,
@@ -976,7 +977,17 @@ int ctg_rag_features(const void* labels, int label_bits, const void* data, int d
         // profiles/r4/ablate)
         if (cols * ((shape[0] + 127) / 128) >= 32768) tz = 128;
         while (tz > 8 && cols * ((shape[0] + tz - 1) / tz) < 1024) tz /= 2;
-        P.tile_z_narrow = std::min(tz, NARROW_TILE_Z);
+        // narrow tiles 16 planes deep, deeper where that would launch more than
+        // 64 K workgroups: both widths are launched and one exits at once, and
+        // at 2048^3 the exiting launch of 16-plane narrow tiles (524 K
+        // workgroups) cost 0.22 ms per call
+        {
+            const int64_t rn = scan_tile_rows_narrow();
+            const int64_t cols_n = ((shape[2] + TILE_X - 1) / TILE_X) * ((shape[1] + rn - 1) / rn);
+            int tzn = std::min(tz, NARROW_TILE_Z);
+            while (tzn < tz && cols_n * ((shape[0] + tzn - 1) / tzn) > 65536) tzn *= 2;
+            P.tile_z_narrow = tzn;
+        }
         if (const char* t = getenv("CTG_TILE_Z")) P.tile_z_narrow = tz = std::max(1, atoi(t));
         if (const char* t = getenv("CTG_TILE_Z_NARROW")) P.tile_z_narrow = std::max(1, atoi(t));
         P.tile_z = tz;

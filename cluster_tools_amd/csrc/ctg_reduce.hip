@@ -69,7 +69,7 @@ __global__ void k_max_pairs(int64_t n, const uint64_t* __restrict__ uv, unsigned
     if ((threadIdx.x & 63) == 0 && m) atomicMax(out, m);
 }
 
-// one narrow 128-byte body at p (HBM or LDS): (S1, S2), the 24 record words, the pivot
+// one narrow 128-byte record body at p: (S1, S2), the 24 record words, the pivot
 __device__ __forceinline__ void add_narrow(const uint4* p, uint32_t (&h)[NSLOTS], uint32_t& cnt, uint32_t& flags,
                                            uint32_t& mn, uint32_t& mx, Moments& mo) {
     const double2 sw = *reinterpret_cast<const double2*>(p);

@@ -1196,6 +1196,7 @@ hipError_t launch_density(const void* L, int label_bits, const int64_t* shape, i
 }
 
 int scan_tile_rows() { return WG_ROWS; }
+int scan_tile_rows_narrow() { return ROWS_NARROW * WAVES; }
 
 // ---------------------------------------------------------------------------
 // unique labels of a box (per-block ``nodes``): LDS hash set per tile
