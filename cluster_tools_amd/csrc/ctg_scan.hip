@@ -257,6 +257,24 @@ __device__ __noinline__ void emit_direct(RecordBuf R, Counters* C, uint64_t key,
     for (int j = NREC_PIV + 1; j < NREC_STRIDE; ++j) b[j] = 0u;
 }
 
+// affinity samples are read once: a non-temporal load keeps them from
+// evicting the label lines the long-range partner gathers re-read from L2
+// (CTG_NT_AFF=0: ordinary loads)
+#ifndef CTG_NT_AFF
+#define CTG_NT_AFF 1
+#endif
+template <typename DataT>
+__device__ __forceinline__ float load_val_stream(const DataT* p, int64_t i) {
+    if constexpr (CTG_NT_AFF == 0) {
+        if constexpr (sizeof(DataT) == 1) return __fdiv_rn((float)p[i], 255.0f);
+        else return p[i];
+    } else if constexpr (sizeof(DataT) == 1) {
+        return __fdiv_rn((float)__builtin_nontemporal_load(p + i), 255.0f);
+    } else {
+        return __builtin_nontemporal_load(p + i);
+    }
+}
+
 template <typename DataT>
 __device__ __forceinline__ float load_val(const DataT* p, int64_t i) {
     if constexpr (sizeof(DataT) == 1) {
@@ -971,7 +989,7 @@ __global__ __launch_bounds__(SCAN_THREADS, CTG_SCAN_MIN_WAVES) void k_face_scan(
                                     // the low half only: every label's high half is
                                     // checked where its own tile loads it
                                     lq[k] = load_lo(L, (int64_t)qz * sz + (int64_t)qy * X + qx);
-                                    av[k] = load_val<DataT>(D, (int64_t)c * Z * sz + iz + (int64_t)r * X);
+                                    av[k] = load_val_stream<DataT>(D, (int64_t)c * Z * sz + iz + (int64_t)r * X);
                                 }
                             }
                         }

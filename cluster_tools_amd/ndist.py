@@ -448,18 +448,52 @@ def _stats_dataset(fo, outKey, shape, chunks):  # noqa: N803
                               compression=comp)
 
 
-def encode_stats_words(sums, records):
-    """(E,2) float64 sums + (E,48) uint32 records -> (E,52) uint32 words."""
+# A block's companion rows come in one of two widths, told apart by the chunk's
+# element count over its edge count: STATS_WORDS (the sums + the 48-word wide
+# record) or, when every histogram slot of the block fits 16 bits and the pad
+# words are zero (always, for rows this library writes), STATS_WORDS_COMPACT:
+# the sums, the 42 slots as u16 pairs, count|ADJ, min, max, pivot -- 116
+# instead of 208 bytes per edge.
+STATS_WORDS_COMPACT = 4 + rag.NSLOTS // 2 + 4
+
+
+def encode_stats_words(sums, records, compact=True):
+    """(E,2) float64 sums + (E,48) uint32 records -> (E,52) uint32 words, or
+    (E,29) when the block's histograms fit 16-bit slots (``compact``)."""
     n = records.shape[0]
+    recs = np.asarray(records, dtype=np.uint32).reshape(n, rag.WIDE_WORDS)
+    sw = np.ascontiguousarray(sums, dtype=np.float64).view(np.uint32).reshape(n, 4)
+    ns = rag.NSLOTS
+    if compact and n and int(recs[:, :ns].max()) <= 0xFFFF and not recs[:, ns + 4:].any():
+        out = np.empty((n, STATS_WORDS_COMPACT), dtype=np.uint32)
+        out[:, :4] = sw
+        out[:, 4:4 + ns // 2] = recs[:, 0:ns:2] | (recs[:, 1:ns:2] << np.uint32(16))
+        out[:, 4 + ns // 2:] = recs[:, ns:ns + 4]
+        return out
     out = np.empty((n, STATS_WORDS), dtype=np.uint32)
-    out[:, :4] = np.ascontiguousarray(sums, dtype=np.float64).view(np.uint32).reshape(n, 4)
-    out[:, 4:] = records
+    out[:, :4] = sw
+    out[:, 4:] = recs
     return out
 
 
-def decode_stats_words(words):
-    w = np.ascontiguousarray(words, dtype=np.uint32).reshape(-1, STATS_WORDS)
-    return np.ascontiguousarray(w[:, :4]).view(np.float64).reshape(-1, 2), np.ascontiguousarray(w[:, 4:])
+def decode_stats_words(words, n_rows=None):
+    """Inverse of encode_stats_words: (sums (E,2) f64, records (E,48) u32); the
+    row width comes from the word count over ``n_rows`` (default: full rows)."""
+    w = np.ascontiguousarray(words, dtype=np.uint32).ravel()
+    width = STATS_WORDS if n_rows is None else (w.size // max(int(n_rows), 1) if n_rows else STATS_WORDS)
+    if width not in (STATS_WORDS, STATS_WORDS_COMPACT) or (n_rows is not None and w.size != width * int(n_rows)):
+        raise RuntimeError('statistics companion: %d words for %s rows' % (w.size, n_rows))
+    w = w.reshape(-1, width)
+    sums = np.ascontiguousarray(w[:, :4]).view(np.float64).reshape(-1, 2)
+    if width == STATS_WORDS:
+        return sums, np.ascontiguousarray(w[:, 4:])
+    ns = rag.NSLOTS
+    recs = np.zeros((w.shape[0], rag.WIDE_WORDS), dtype=np.uint32)
+    h = w[:, 4:4 + ns // 2]
+    recs[:, 0:ns:2] = h & np.uint32(0xFFFF)
+    recs[:, 1:ns:2] = h >> np.uint32(16)
+    recs[:, ns:ns + 4] = w[:, 4 + ns // 2:]
+    return sums, recs
 
 
 def _write_block_features(fo, outKey, pos, shape, chunks, feats, sums, records):  # noqa: N803
@@ -773,7 +807,7 @@ def mergeFeatureBlocks(graphPath, subgraphKey, featuresPath, featuresKey, outPat
         have_stats = featuresKey + STATS_SUFFIX in ff
         ds_feat = ff[featuresKey + STATS_SUFFIX] if have_stats else ff[featuresKey]
         n_features = int(ff[featuresKey].attrs.get('n_features', N_FEATURES))
-        width = STATS_WORDS if have_stats else n_features
+        width = n_features   # (companion rows: per block, decode_stats_words)
 
         block_ids = [int(b) for b in blockIds]
         positions = [blk.blockGridPosition(b) for b in block_ids]
@@ -782,7 +816,13 @@ def mergeFeatureBlocks(graphPath, subgraphKey, featuresPath, featuresKey, outPat
         for b, ids, rows in zip(block_ids, all_ids, all_rows):
             if ids is None or rows is None:
                 continue
-            rows = rows.reshape(-1, width)
+            if have_stats:   # one canonical width for the concatenation
+                if rows.size not in (ids.shape[0] * STATS_WORDS, ids.shape[0] * STATS_WORDS_COMPACT):
+                    raise RuntimeError('mergeFeatureBlocks: block %d has %d edge ids but %d statistics words'
+                                       % (b, ids.shape[0], rows.size))
+                sm, rc = decode_stats_words(rows, ids.shape[0])
+                rows = encode_stats_words(sm, rc, compact=False)
+            rows = rows.reshape(-1, STATS_WORDS if have_stats else width)
             if rows.shape[0] != ids.shape[0]:
                 raise RuntimeError('mergeFeatureBlocks: block %d has %d edge ids but %d feature rows'
                                    % (b, ids.shape[0], rows.shape[0]))

@@ -18,6 +18,7 @@ from . import _lib as L
 N_FEATURES = L.CTG_N_FEATURES
 NBINS = L.CTG_NBINS
 WIDE_WORDS = L.CTG_WIDE_RECORD_WORDS
+NSLOTS = NBINS + 2   # histogram slots of a wide record: left outliers, the bins, right outliers
 
 
 def _is_torch(x):

@@ -272,6 +272,33 @@ def test_stats_companion_words_roundtrip():
     np.testing.assert_array_equal(r2, recs)
 
 
+def test_stats_companion_compact_rows():
+    """Blocks whose histogram slots fit 16 bits (and whose pad words are zero,
+    as the library writes them) store 29-word rows; decode detects the width
+    from the word count and restores the 48-word records exactly; a block with
+    a slot above 65535 keeps the 52-word rows."""
+    from cluster_tools_amd import ndist
+    rng = np.random.default_rng(2)
+    n = 9
+    sums = rng.random((n, 2))
+    recs = np.zeros((n, 48), np.uint32)
+    recs[:, :42] = rng.integers(0, 65536, (n, 42))
+    recs[:, 42] = rng.integers(1, 2 ** 31, n) | np.uint32(0x80000000)
+    recs[:, 43:46] = rng.integers(0, 2 ** 32, (n, 3), dtype=np.uint64).astype(np.uint32)
+    w = ndist.encode_stats_words(sums, recs)
+    assert w.shape == (n, ndist.STATS_WORDS_COMPACT) == (n, 29)
+    s2, r2 = ndist.decode_stats_words(w.ravel(), n)
+    np.testing.assert_array_equal(s2, sums)
+    np.testing.assert_array_equal(r2, recs)
+    recs[3, 17] = 65536
+    w = ndist.encode_stats_words(sums, recs)
+    assert w.shape == (n, ndist.STATS_WORDS)
+    s2, r2 = ndist.decode_stats_words(w.ravel(), n)
+    np.testing.assert_array_equal(r2, recs)
+    with pytest.raises(RuntimeError):
+        ndist.decode_stats_words(w.ravel()[:-1], n)
+
+
 def test_blocks_in_volume_block_list_path(tmp_path):
     lp = tmp_path / 'blocks.json'
     lp.write_text(json.dumps([1, 9, 11, 12]))
