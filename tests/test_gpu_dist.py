@@ -117,7 +117,7 @@ def test_rccl_world1_exchange_equals_single_call(tmp_path, affinity):
     assert list(np.load(tmp_path / 'reads.npy')) == ['counts', 'counts', 'offsets']
 
 
-@pytest.mark.parametrize('affinity', [False, True])
+@pytest.mark.parametrize('affinity', [False, True, 'lr'])
 def test_mgpu_exchange_simulated_in_one_process(affinity):
     """ctg_mgpu_sample / split / pack / merge of every rank in one process
     (tests/exchange_sim.py: the collectives replaced by their data movement)
@@ -129,7 +129,9 @@ def test_mgpu_exchange_simulated_in_one_process(affinity):
     from cluster_tools_amd import synthetic
     from tests.dist_helpers import splitters, split_counts, Part
     from tests.exchange_sim import simulate
-    offs = synthetic.NN_OFFSETS if affinity else None
+    # 'lr': test_mws.py's 12 long-range offsets -- slabs with 4 halo planes, and
+    # non-adjacent pairs kept by every rank until the merged ADJ bits decide
+    offs = synthetic.LR_OFFSETS if affinity == 'lr' else synthetic.NN_OFFSETS if affinity else None
     lab, bnd = rag.synth_volume(SHAPE, cell=7, seed=9)
     data = rag.synth_affinities(bnd, offs) if affinity else bnd
     ref = rag.rag_features(lab.cpu().numpy().view(np.uint64), data.cpu().numpy(), offsets=offs)
