@@ -302,8 +302,14 @@ def rag_features_distributed(labels, data=None, offsets=None, own_begin=None, ow
         loc.free()
     # the global offsets: every rank's shard sizes, gathered now (collective
     # order), read by the host on first use (DistResult)
-    sizes = all_gather_flat(torch.tensor([int(shard.n_edges), int(shard.n_nodes)], dtype=torch.int64,
-                                         device=wire), group)
+    ne, nn = int(shard.n_edges), int(shard.n_nodes)
+    if wire.type == 'cuda':
+        # built on the device by one kernel (no pageable host -> device copy,
+        # which would wait for the stream)
+        mine = torch.arange(2, dtype=torch.int64, device=wire) * (nn - ne) + ne
+    else:
+        mine = torch.tensor([ne, nn], dtype=torch.int64)
+    sizes = all_gather_flat(mine, group)
     phase('offsets')
     return DistResult(shard, sizes, rank, info)
 
