@@ -1081,6 +1081,21 @@ int ctg_rag_features(const void* labels, int label_bits, const void* data, int d
         P.skip_adj_marks = P.n_channels > 0 && nn[0] && nn[1] && nn[2] && !(flags & CTG_NO_ADJ_FILTER) &&
                            (!long_range || P.bloom != nullptr);
         if (const char* sa = getenv("CTG_SKIP_ADJ")) P.skip_adj_marks = P.skip_adj_marks && atoi(sa);
+        // exactly the three nearest-neighbour channels (any order), every
+        // sample an adjacency proof: the face-scan form of the affinity scan
+        // (MODE_AFF_NN, ctg_scan.hip); CTG_NN3=0 keeps the channel loop
+        if (P.n_channels == 3 && !long_range && P.skip_adj_marks) {
+            int ch[3] = {-1, -1, -1};
+            for (int c = 0; c < 3; ++c)
+                for (int a = 0; a < 3; ++a)
+                    if (P.offsets[c][a] == -1 && P.offsets[c][(a + 1) % 3] == 0 && P.offsets[c][(a + 2) % 3] == 0)
+                        ch[a] = c;
+            const char* e = getenv("CTG_NN3");
+            if (ch[0] >= 0 && ch[1] >= 0 && ch[2] >= 0 && !(e && e[0] == '0')) {
+                P.nn3 = 1;
+                for (int a = 0; a < 3; ++a) P.nn_ch[a] = ch[a];
+            }
+        }
     }
     struct AdjRelease {   // the set and its graph live until the scan is done
         unsigned long long*& set;

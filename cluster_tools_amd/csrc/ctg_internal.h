@@ -166,6 +166,11 @@ struct ScanParams {
     // RAG edge gets a sample of one of them and the scan pushes no adjacency
     // markers (with a Bloom filter those samples carry the flag instead)
     int skip_adj_marks;
+    // the three nearest-neighbour channels alone (whole array, no long-range
+    // channel, adjacency proven by every sample): scanned as faces, like a
+    // boundary map, the sample of face (p - e_a, p) being aff[nn_ch[a], p]
+    int nn3;
+    int nn_ch[3];              // channel of the offset -e_a, a = z, y, x
     uint32_t lr_mask;          // bit c: channel c is long-range (|offset|_1 > 1)
     int narrow_rows;           // boundary maps: 1 2-row waves (fragmented volumes, see ctg_scan.hip),
                                // 2 decided on the device from density[] (no host round trip)

@@ -41,7 +41,7 @@
 
 namespace ctg {
 
-enum { MODE_GRAPH = 0, MODE_BOUNDARY = 1, MODE_AFFINITY = 2 };
+enum { MODE_GRAPH = 0, MODE_BOUNDARY = 1, MODE_AFFINITY = 2, MODE_AFF_NN = 3 };
 
 // y rows per wave, held in registers: 4, or 2 for highly fragmented volumes
 // (the workgroup's tile cross-section, hence its live edge set, halves: the
@@ -658,6 +658,7 @@ template <typename LabelT, typename DataT, int MODE, bool FAST40, bool BATCH, in
 __global__ __launch_bounds__(SCAN_THREADS, CTG_SCAN_MIN_WAVES) void k_face_scan(ScanParams P, RecordBuf R, Counters* C) {
     constexpr bool BND = MODE == MODE_BOUNDARY;
     constexpr bool AFF = MODE == MODE_AFFINITY;
+    constexpr bool NN3 = MODE == MODE_AFF_NN;   // nearest-neighbour affinities scanned as faces (P.nn3)
     constexpr bool STATS = MODE != MODE_GRAPH;
     using StageT = typename std::conditional<STATS, uint4, uint2>::type;
     __shared__ Table T;
@@ -793,6 +794,10 @@ __global__ __launch_bounds__(SCAN_THREADS, CTG_SCAN_MIN_WAVES) void k_face_scan(
     uint32_t Lc[ROWS + 1];
     LabelT Ln[ROWS + 1];
     float Dc[ROWS + 1], Dn[ROWS + 1];
+    // NN3: Dc / Dn hold the x channel; the y channel's rows (sample of face
+    // (y, y+1) = row r + 1) and the prefetched plane's z channel (sample of
+    // face (z, z+1) = plane z + 1)
+    float Dyc[ROWS + 1], Dyn[ROWS + 1], Dzn[ROWS];
     uint32_t XLc = 0;
     LabelT XLn = 0;
     float XDc = 0.f, XDn = 0.f;
@@ -809,22 +814,35 @@ __global__ __launch_bounds__(SCAN_THREADS, CTG_SCAN_MIN_WAVES) void k_face_scan(
     // branches and no default moves sit between the loads.
     const int xcl = min(x, X - 1);
     const int xhc = min(xh, X - 1);
-    auto load_plane = [&](int z, LabelT (&Lb)[ROWS + 1], float (&Db)[ROWS + 1], LabelT& XL, float& XD) {
+    const int64_t csz = (int64_t)Z * sz;   // channel stride (NN3)
+    auto load_plane = [&](int z, LabelT (&Lb)[ROWS + 1], float (&Db)[ROWS + 1], LabelT& XL, float& XD,
+                          float (&Dyb)[ROWS + 1], float (&Dzb)[ROWS], bool with_z) {
         const LabelT* Lz = L + (int64_t)z * sz + (int64_t)yw * X;
-        const DataT* Dz = BND ? D + (int64_t)z * sz + (int64_t)yw * X : nullptr;
+        const DataT* Dz = BND ? D + (int64_t)z * sz + (int64_t)yw * X
+                              : NN3 ? D + (int64_t)P.nn_ch[2] * csz + (int64_t)z * sz + (int64_t)yw * X : nullptr;
         const int rmax = Y - 1 - yw;   // last valid row offset (uniform; < 0 only for waves past Y)
 #pragma unroll
         for (int r = 0; r <= ROWS; ++r) {
             const int rr = min(r, rmax);
             Lb[r] = Lz[(int64_t)rr * X + xcl];
-            if constexpr (BND) Db[r] = load_val<DataT>(Dz, (int64_t)rr * X + xcl);
+            if constexpr (BND || NN3) Db[r] = load_val<DataT>(Dz, (int64_t)rr * X + xcl);
             else Db[r] = 0.f;
+        }
+        if constexpr (NN3) {
+            const DataT* Ay = D + (int64_t)P.nn_ch[1] * csz + (int64_t)z * sz + (int64_t)yw * X;
+            const DataT* Az = D + (int64_t)P.nn_ch[0] * csz + (int64_t)z * sz + (int64_t)yw * X;
+#pragma unroll
+            for (int r = 1; r <= ROWS; ++r) Dyb[r] = load_val_stream<DataT>(Ay, (int64_t)min(r, rmax) * X + xcl);
+            if (with_z) {
+#pragma unroll
+                for (int r = 0; r < ROWS; ++r) Dzb[r] = load_val_stream<DataT>(Az, (int64_t)min(r, rmax) * X + xcl);
+            }
         }
         // x-halo: lane r < ROWS holds row r's voxel at x = x0 + 64 (lanes past
         // ROWS repeat row ROWS - 1; only lanes < ROWS are read)
         const int hr = min(min(lane, ROWS - 1), rmax);
         XL = Lz[(int64_t)hr * X + xhc];
-        if constexpr (BND) XD = load_val<DataT>(Dz, (int64_t)hr * X + xhc);
+        if constexpr (BND || NN3) XD = load_val<DataT>(Dz, (int64_t)hr * X + xhc);
         else XD = 0.f;
     };
 
@@ -899,7 +917,7 @@ __global__ __launch_bounds__(SCAN_THREADS, CTG_SCAN_MIN_WAVES) void k_face_scan(
     } while (0)
 
     if (z0 < z1) {
-        load_plane(z0, Ln, Dc, XLn, XDc);
+        load_plane(z0, Ln, Dc, XLn, XDc, Dyc, Dzn, false);
 #pragma unroll
         for (int r = 0; r <= ROWS; ++r) Lc[r] = narrow(Ln[r]);
         XLc = narrow(XLn);
@@ -913,7 +931,7 @@ __global__ __launch_bounds__(SCAN_THREADS, CTG_SCAN_MIN_WAVES) void k_face_scan(
         // (Tried: z faces (z-1, z) against the previous plane, so nothing in
         // a plane waits for the prefetch -- 0.006 ms faster at 512^3, but the
         // changed face order raised records by 23 % at cell 5.)
-        load_plane(hz ? z + 1 : z, Ln, Dn, XLn, XDn);
+        load_plane(hz ? z + 1 : z, Ln, Dn, XLn, XDn, Dyn, Dzn, true);
         const bool zlo = z >= obz && z < oez;
         const bool zup = hz && z + 1 >= obz && z + 1 < oez;      // face (z, z+1): upper voxel in the own box
         const bool zg = batch && z >= gbz && z < gez;            // graph box planes (batched)
@@ -942,22 +960,31 @@ __global__ __launch_bounds__(SCAN_THREADS, CTG_SCAN_MIN_WAVES) void k_face_scan(
                 // does not own go in as adjacency-only entries
                 const bool xo = (s_xo >> r) & 1u, xg = BATCH && ((s_xg >> r) & 1u);
                 if ((xo || xg) && (!AFF || adj_marks)) {
-                    const float dx = BND ? __uint_as_float(shl1(__float_as_uint(Dc[r]),
-                                                                (uint32_t)__builtin_amdgcn_readlane(
-                                                                    (int)__float_as_uint(XDc), r)))
-                                         : 0.f;
+                    const float dx = (BND || NN3) ? __uint_as_float(shl1(__float_as_uint(Dc[r]),
+                                                                         (uint32_t)__builtin_amdgcn_readlane(
+                                                                             (int)__float_as_uint(XDc), r)))
+                                                  : 0.f;
                     const bool own = xo && lane_xf;
-                    PUSH(lc != lx, (xo ? m_xf : 0ull) | (xg ? m_gxf : 0ull), own || (xg && glane_xf), lc, lx, (own || !BATCH) ? __float_as_uint(Dc[r]) : MARK_ADJ,
-                         (AFF || (BATCH && !own)) ? MARK_ADJ : __float_as_uint(dx));
+                    if constexpr (NN3) {   // aff[x channel] of the upper voxel x + 1
+                        PUSH(lc != lx, m_xf, own, lc, lx, __float_as_uint(dx), MARK_ONE);
+                    } else {
+                        PUSH(lc != lx, (xo ? m_xf : 0ull) | (xg ? m_gxf : 0ull), own || (xg && glane_xf), lc, lx,
+                             (own || !BATCH) ? __float_as_uint(Dc[r]) : MARK_ADJ,
+                             (AFF || (BATCH && !own)) ? MARK_ADJ : __float_as_uint(dx));
+                    }
                 }
                 // y face (y, y+1)
                 const bool yo = (s_yo >> r) & 1u, yg = BATCH && ((s_yg >> r) & 1u);
                 if ((yo || yg) && (!AFF || adj_marks)) {
                     const bool own = yo && lane_yz;
-                    PUSH(lc != Lc[r + 1], (yo ? m_yz : 0ull) | (yg ? m_gyz : 0ull), own || (yg && glane_yz), lc,
-                         Lc[r + 1],
-                         (own || !BATCH) ? __float_as_uint(Dc[r]) : MARK_ADJ,
-                         (AFF || (BATCH && !own)) ? MARK_ADJ : __float_as_uint(Dc[r + 1]));
+                    if constexpr (NN3) {   // aff[y channel] of the upper voxel, row r + 1
+                        PUSH(lc != Lc[r + 1], m_yz, own, lc, Lc[r + 1], __float_as_uint(Dyc[r + 1]), MARK_ONE);
+                    } else {
+                        PUSH(lc != Lc[r + 1], (yo ? m_yz : 0ull) | (yg ? m_gyz : 0ull), own || (yg && glane_yz), lc,
+                             Lc[r + 1],
+                             (own || !BATCH) ? __float_as_uint(Dc[r]) : MARK_ADJ,
+                             (AFF || (BATCH && !own)) ? MARK_ADJ : __float_as_uint(Dc[r + 1]));
+                    }
                 }
             }
             // affinity samples aff[c, p] for q = p + o_c, p in the owned box:
@@ -1058,9 +1085,13 @@ __global__ __launch_bounds__(SCAN_THREADS, CTG_SCAN_MIN_WAVES) void k_face_scan(
                     if (zo || zgr) {
                         const bool own = zo && lane_yz;
                         const uint32_t ln = (uint32_t)Ln[r];
-                        PUSH(Lc[r] != ln, (zo ? m_yz : 0ull) | (zgr ? m_gyz : 0ull), own || (zgr && glane_yz),
-                             Lc[r], ln, (own || !BATCH) ? __float_as_uint(Dc[r]) : MARK_ADJ,
-                             (AFF || (BATCH && !own)) ? MARK_ADJ : __float_as_uint(Dn[r]));
+                        if constexpr (NN3) {   // aff[z channel] of the upper voxel, plane z + 1
+                            PUSH(Lc[r] != ln, m_yz, own, Lc[r], ln, __float_as_uint(Dzn[r]), MARK_ONE);
+                        } else {
+                            PUSH(Lc[r] != ln, (zo ? m_yz : 0ull) | (zgr ? m_gyz : 0ull), own || (zgr && glane_yz),
+                                 Lc[r], ln, (own || !BATCH) ? __float_as_uint(Dc[r]) : MARK_ADJ,
+                                 (AFF || (BATCH && !own)) ? MARK_ADJ : __float_as_uint(Dn[r]));
+                        }
                     }
                 }
             }
@@ -1077,6 +1108,9 @@ __global__ __launch_bounds__(SCAN_THREADS, CTG_SCAN_MIN_WAVES) void k_face_scan(
         for (int r = 0; r <= ROWS; ++r) {
             Lc[r] = narrow(Ln[r]);
             Dc[r] = Dn[r];
+            if constexpr (NN3) {
+                if (r >= 1) Dyc[r] = Dyn[r];   // (row 0 of the y channel is never a sample)
+            }
         }
         XLc = narrow(XLn);
         XDc = XDn;
@@ -1165,11 +1199,14 @@ static hipError_t launch_scan_l(const ScanParams& P, const RecordBuf& R, Counter
     if (P.data_kind == CTG_DATA_NONE || P.data == nullptr)
         return launch_scan_t<LabelT, float, MODE_GRAPH>(P, R, C, s);
     const bool aff = P.n_channels > 0;
+    const bool nn3 = aff && P.nn3 && !P.blocks;
     if (P.data_kind == CTG_DATA_U8)
-        return aff ? launch_scan_t<LabelT, uint8_t, MODE_AFFINITY>(P, R, C, s)
-                   : launch_scan_t<LabelT, uint8_t, MODE_BOUNDARY>(P, R, C, s);
-    return aff ? launch_scan_t<LabelT, float, MODE_AFFINITY>(P, R, C, s)
-               : launch_scan_t<LabelT, float, MODE_BOUNDARY>(P, R, C, s);
+        return nn3 ? launch_scan_t<LabelT, uint8_t, MODE_AFF_NN>(P, R, C, s)
+               : aff ? launch_scan_t<LabelT, uint8_t, MODE_AFFINITY>(P, R, C, s)
+                     : launch_scan_t<LabelT, uint8_t, MODE_BOUNDARY>(P, R, C, s);
+    return nn3 ? launch_scan_t<LabelT, float, MODE_AFF_NN>(P, R, C, s)
+           : aff ? launch_scan_t<LabelT, float, MODE_AFFINITY>(P, R, C, s)
+                 : launch_scan_t<LabelT, float, MODE_BOUNDARY>(P, R, C, s);
 }
 
 hipError_t launch_face_scan(const ScanParams& P, const RecordBuf& R, Counters* C, hipStream_t s) {
