@@ -1096,6 +1096,24 @@ int ctg_rag_features(const void* labels, int label_bits, const void* data, int d
                 for (int a = 0; a < 3; ++a) P.nn_ch[a] = ch[a];
             }
         }
+        // long-range calls with the Bloom filter: the nearest-neighbour
+        // channels as faces (their samples flag adjacency), the rest looped
+        if (long_range && P.bloom != nullptr && P.skip_adj_marks) {
+            int ch[3] = {-1, -1, -1};
+            for (int c = 0; c < P.n_channels; ++c)
+                for (int a = 0; a < 3; ++a)
+                    if (ch[a] < 0 && P.offsets[c][a] == -1 && P.offsets[c][(a + 1) % 3] == 0 &&
+                        P.offsets[c][(a + 2) % 3] == 0)
+                        ch[a] = c;
+            const char* e = getenv("CTG_NN3");
+            if (ch[0] >= 0 && ch[1] >= 0 && ch[2] >= 0 && !(e && e[0] == '0')) {
+                P.nn_mix = 1;
+                for (int a = 0; a < 3; ++a) P.nn_ch[a] = ch[a];
+                P.n_loop = 0;
+                for (int c = 0; c < P.n_channels; ++c)
+                    if (c != ch[0] && c != ch[1] && c != ch[2]) P.loop_ch[P.n_loop++] = c;
+            }
+        }
     }
     struct AdjRelease {   // the set and its graph live until the scan is done
         unsigned long long*& set;

@@ -171,6 +171,12 @@ struct ScanParams {
     // boundary map, the sample of face (p - e_a, p) being aff[nn_ch[a], p]
     int nn3;
     int nn_ch[3];              // channel of the offset -e_a, a = z, y, x
+    // long-range calls (Bloom-filtered): the three nearest-neighbour channels
+    // as faces (their samples are the adjacency proofs), the other channels
+    // loop_ch[0 .. n_loop) in the channel loop
+    int nn_mix;
+    int n_loop;
+    int loop_ch[CTG_MAX_CHANNELS];
     uint32_t lr_mask;          // bit c: channel c is long-range (|offset|_1 > 1)
     int narrow_rows;           // boundary maps: 1 2-row waves (fragmented volumes, see ctg_scan.hip),
                                // 2 decided on the device from density[] (no host round trip)

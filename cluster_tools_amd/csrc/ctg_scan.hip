@@ -41,7 +41,7 @@
 
 namespace ctg {
 
-enum { MODE_GRAPH = 0, MODE_BOUNDARY = 1, MODE_AFFINITY = 2, MODE_AFF_NN = 3 };
+enum { MODE_GRAPH = 0, MODE_BOUNDARY = 1, MODE_AFFINITY = 2, MODE_AFF_NN = 3, MODE_AFF_MIX = 4 };
 
 // y rows per wave, held in registers: 4, or 2 for highly fragmented volumes
 // (the workgroup's tile cross-section, hence its live edge set, halves: the
@@ -389,7 +389,7 @@ template <int MODE, bool FAST40, bool BATCH, typename StageT>
 __device__ __forceinline__ void fold_stats(Table& T, const StageT& e, int s, uint32_t pv, RecordBuf R, Counters* C,
                                            double scale, double offset, bool& need, int ablate) {
     constexpr bool BND = MODE == MODE_BOUNDARY;
-    constexpr bool AFF = MODE == MODE_AFFINITY;
+    constexpr bool AFF = MODE == MODE_AFFINITY || MODE == MODE_AFF_MIX;
     const uint64_t key = ((uint64_t)e.x << 32) | e.y;
     if constexpr (MODE == MODE_GRAPH) {
         if (s < 0) emit_direct(R, C, key, 0u, -1, -1, 0.0, 0.0, 0u, 0u, 0u, false);
@@ -493,7 +493,7 @@ __device__ __forceinline__ void fold_grouped(Table& T, const StageT (&e)[NPER], 
                                              const uint32_t (&pv)[NPER], int lane, RecordBuf R, Counters* C,
                                              double scale, double offset, int ablate) {
     constexpr bool BND = MODE == MODE_BOUNDARY;
-    constexpr bool AFF = MODE == MODE_AFFINITY;
+    constexpr bool AFF = MODE == MODE_AFFINITY || MODE == MODE_AFF_MIX;
 #pragma unroll
     for (int i = 0; i < NPER; ++i) {
         const int sl = slot[i];
@@ -657,8 +657,11 @@ template <typename LabelT, typename DataT, int MODE, bool FAST40, bool BATCH, in
 #endif
 __global__ __launch_bounds__(SCAN_THREADS, CTG_SCAN_MIN_WAVES) void k_face_scan(ScanParams P, RecordBuf R, Counters* C) {
     constexpr bool BND = MODE == MODE_BOUNDARY;
-    constexpr bool AFF = MODE == MODE_AFFINITY;
+    constexpr bool AFF = MODE == MODE_AFFINITY || MODE == MODE_AFF_MIX;
     constexpr bool NN3 = MODE == MODE_AFF_NN;   // nearest-neighbour affinities scanned as faces (P.nn3)
+    constexpr bool MIX = MODE == MODE_AFF_MIX;  // ... and the long-range channels in the loop (P.nn_mix)
+    constexpr bool NNF = NN3 || MIX;            // faces carry the nearest-neighbour channels' samples
+    constexpr uint32_t NN_MARK = MIX ? MARK_ONE_ADJ : MARK_ONE;   // MIX: each such sample proves adjacency
     constexpr bool STATS = MODE != MODE_GRAPH;
     using StageT = typename std::conditional<STATS, uint4, uint2>::type;
     __shared__ Table T;
@@ -945,6 +948,20 @@ __global__ __launch_bounds__(SCAN_THREADS, CTG_SCAN_MIN_WAVES) void k_face_scan(
         const uint32_t s_xg = (uint32_t)__builtin_amdgcn_readfirstlane((int)(zg ? grow_x : 0u));
         const uint32_t s_yg = (uint32_t)__builtin_amdgcn_readfirstlane((int)(zg ? grow_y : 0u));
         const uint32_t s_zg = (uint32_t)__builtin_amdgcn_readfirstlane((int)(gzup ? grow_x : 0u));
+        if constexpr (MIX) {
+            // the channel loop holds most registers: the nearest-neighbour
+            // channels of this plane are loaded here, not prefetched with the
+            // labels, and die before the loop (x channel rows + x-halo, y
+            // channel rows 1..ROWS); the z channel is loaded before the z faces
+            const int rmax = Y - 1 - yw;
+            const DataT* Ax = D + (int64_t)P.nn_ch[2] * csz + (int64_t)z * sz + (int64_t)yw * X;
+            const DataT* Ay = D + (int64_t)P.nn_ch[1] * csz + (int64_t)z * sz + (int64_t)yw * X;
+#pragma unroll
+            for (int r = 0; r < ROWS; ++r) Dc[r] = load_val_stream<DataT>(Ax, (int64_t)min(r, rmax) * X + xcl);
+            XDc = load_val<DataT>(Ax, (int64_t)min(min(lane, ROWS - 1), rmax) * X + xhc);
+#pragma unroll
+            for (int r = 1; r <= ROWS; ++r) Dyc[r] = load_val_stream<DataT>(Ay, (int64_t)min(r, rmax) * X + xcl);
+        }
         if (ablate & 8) {   // diagnostic: loads only
             uint32_t chk = 0;
 #pragma unroll
@@ -959,14 +976,14 @@ __global__ __launch_bounds__(SCAN_THREADS, CTG_SCAN_MIN_WAVES) void k_face_scan(
                 // owned faces carry samples; (batched) sub-graph faces the block
                 // does not own go in as adjacency-only entries
                 const bool xo = (s_xo >> r) & 1u, xg = BATCH && ((s_xg >> r) & 1u);
-                if ((xo || xg) && (!AFF || adj_marks)) {
-                    const float dx = (BND || NN3) ? __uint_as_float(shl1(__float_as_uint(Dc[r]),
+                if ((xo || xg) && (!AFF || adj_marks || NNF)) {
+                    const float dx = (BND || NNF) ? __uint_as_float(shl1(__float_as_uint(Dc[r]),
                                                                          (uint32_t)__builtin_amdgcn_readlane(
                                                                              (int)__float_as_uint(XDc), r)))
                                                   : 0.f;
                     const bool own = xo && lane_xf;
-                    if constexpr (NN3) {   // aff[x channel] of the upper voxel x + 1
-                        PUSH(lc != lx, m_xf, own, lc, lx, __float_as_uint(dx), MARK_ONE);
+                    if constexpr (NNF) {   // aff[x channel] of the upper voxel x + 1
+                        PUSH(lc != lx, m_xf, own, lc, lx, __float_as_uint(dx), NN_MARK);
                     } else {
                         PUSH(lc != lx, (xo ? m_xf : 0ull) | (xg ? m_gxf : 0ull), own || (xg && glane_xf), lc, lx,
                              (own || !BATCH) ? __float_as_uint(Dc[r]) : MARK_ADJ,
@@ -975,10 +992,10 @@ __global__ __launch_bounds__(SCAN_THREADS, CTG_SCAN_MIN_WAVES) void k_face_scan(
                 }
                 // y face (y, y+1)
                 const bool yo = (s_yo >> r) & 1u, yg = BATCH && ((s_yg >> r) & 1u);
-                if ((yo || yg) && (!AFF || adj_marks)) {
+                if ((yo || yg) && (!AFF || adj_marks || NNF)) {
                     const bool own = yo && lane_yz;
-                    if constexpr (NN3) {   // aff[y channel] of the upper voxel, row r + 1
-                        PUSH(lc != Lc[r + 1], m_yz, own, lc, Lc[r + 1], __float_as_uint(Dyc[r + 1]), MARK_ONE);
+                    if constexpr (NNF) {   // aff[y channel] of the upper voxel, row r + 1
+                        PUSH(lc != Lc[r + 1], m_yz, own, lc, Lc[r + 1], __float_as_uint(Dyc[r + 1]), NN_MARK);
                     } else {
                         PUSH(lc != Lc[r + 1], (yo ? m_yz : 0ull) | (yg ? m_gyz : 0ull), own || (yg && glane_yz), lc,
                              Lc[r + 1],
@@ -993,15 +1010,16 @@ __global__ __launch_bounds__(SCAN_THREADS, CTG_SCAN_MIN_WAVES) void k_face_scan(
             if constexpr (AFF) {
                 if (zlo && row_x) {
                     const int64_t iz = (int64_t)z * sz + (int64_t)yw * X + x;
-                    for (int c0 = 0; c0 < P.n_channels; c0 += AFF_G) {
+                    const int n_loop = MIX ? P.n_loop : P.n_channels;
+                    for (int c0 = 0; c0 < n_loop; c0 += AFF_G) {
                         constexpr int K = AFF_G * ROWS;   // (channel, row) sites of the group
                         uint32_t lq[K];
                         float av[K];
                         bool act[K];
 #pragma unroll
                         for (int j = 0; j < AFF_G; ++j) {
-                            const int c = c0 + j;
-                            const bool has = c < P.n_channels;
+                            const bool has = c0 + j < n_loop;
+                            const int c = MIX ? (has ? P.loop_ch[c0 + j] : 0) : c0 + j;
                             const int qz = has ? z + P.offsets[c][0] : -1, oy = has ? P.offsets[c][1] : 0;
                             const int qx = has ? x + P.offsets[c][2] : -1;
                             const bool okzx = lane_yz && qz >= 0 && qz < Z && qx >= 0 && qx < X;
@@ -1023,7 +1041,8 @@ __global__ __launch_bounds__(SCAN_THREADS, CTG_SCAN_MIN_WAVES) void k_face_scan(
 #pragma unroll
                         for (int k = 0; k < K; ++k) act[k] = act[k] && lq[k] != Lc[k % ROWS];
                         // long-range channels: only pairs that are RAG edges
-                        const uint32_t glr = (P.lr_mask >> c0) & ((1u << AFF_G) - 1u);
+                        // (MIX: every loop channel is long-range)
+                        const uint32_t glr = MIX ? (1u << AFF_G) - 1u : (P.lr_mask >> c0) & ((1u << AFF_G) - 1u);
                         if (glr && P.bloom != nullptr && !(ablate & 512)) {
                             uint64_t hb[K];
                             unsigned long long wb[K];
@@ -1042,7 +1061,7 @@ __global__ __launch_bounds__(SCAN_THREADS, CTG_SCAN_MIN_WAVES) void k_face_scan(
                         }
 #pragma unroll
                         for (int j = 0; j < AFF_G; ++j) {
-                            if (c0 + j >= P.n_channels) break;
+                            if (c0 + j >= n_loop) break;
                             const uint32_t mk = (P.bloom != nullptr && !(glr >> j & 1u)) ? MARK_ONE_ADJ : MARK_ONE;
                             // (nearest-neighbour channels unpaired: A/B nn1024 scan 8.6 -> 9.4 ms paired)
                             if (mk == MARK_ONE && P.bloom != nullptr) {
@@ -1072,21 +1091,27 @@ __global__ __launch_bounds__(SCAN_THREADS, CTG_SCAN_MIN_WAVES) void k_face_scan(
                     }
                 }
             }
+            if constexpr (MIX) {   // the z channel of plane z + 1 (upper voxels of the z faces)
+                const int rmax = Y - 1 - yw;
+                const DataT* Az = D + (int64_t)P.nn_ch[0] * csz + (int64_t)(hz ? z + 1 : z) * sz + (int64_t)yw * X;
+#pragma unroll
+                for (int r = 0; r < ROWS; ++r) Dzn[r] = load_val_stream<DataT>(Az, (int64_t)min(r, rmax) * X + xcl);
+            }
             // z faces (z, z+1): plane z against the prefetched plane
             if (stamps) {   // diagnostic: how long the prefetched plane keeps this wave waiting
                 const uint64_t tw = stamp_now();
                 __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
                 t_wait += stamp_now() - tw;
             }
-            if ((s_zo | s_zg) && (!AFF || adj_marks)) {
+            if ((s_zo | s_zg) && (!AFF || adj_marks || NNF)) {
 #pragma unroll
                 for (int r = 0; r < ROWS; ++r) {
                     const bool zo = (s_zo >> r) & 1u, zgr = BATCH && ((s_zg >> r) & 1u);
                     if (zo || zgr) {
                         const bool own = zo && lane_yz;
                         const uint32_t ln = (uint32_t)Ln[r];
-                        if constexpr (NN3) {   // aff[z channel] of the upper voxel, plane z + 1
-                            PUSH(Lc[r] != ln, m_yz, own, Lc[r], ln, __float_as_uint(Dzn[r]), MARK_ONE);
+                        if constexpr (NNF) {   // aff[z channel] of the upper voxel, plane z + 1
+                            PUSH(Lc[r] != ln, m_yz, own, Lc[r], ln, __float_as_uint(Dzn[r]), NN_MARK);
                         } else {
                             PUSH(Lc[r] != ln, (zo ? m_yz : 0ull) | (zgr ? m_gyz : 0ull), own || (zgr && glane_yz),
                                  Lc[r], ln, (own || !BATCH) ? __float_as_uint(Dc[r]) : MARK_ADJ,
@@ -1189,7 +1214,7 @@ static hipError_t launch_scan_t(const ScanParams& P, const RecordBuf& R, Counter
         if (P.narrow_rows == 1 && !P.blocks) return launch_scan_r<LabelT, DataT, MODE, ROWS_NARROW>(P, R, C, s);
     }
     // (batched blocks keep the wide tile: their tile counts come from scan_tile_rows())
-    if constexpr (MODE == MODE_AFFINITY)
+    if constexpr (MODE == MODE_AFFINITY || MODE == MODE_AFF_MIX)
         if (!P.blocks) return launch_scan_r<LabelT, DataT, MODE, ROWS_AFF>(P, R, C, s);
     return launch_scan_r<LabelT, DataT, MODE, ROWS_WIDE>(P, R, C, s);
 }
@@ -1200,11 +1225,14 @@ static hipError_t launch_scan_l(const ScanParams& P, const RecordBuf& R, Counter
         return launch_scan_t<LabelT, float, MODE_GRAPH>(P, R, C, s);
     const bool aff = P.n_channels > 0;
     const bool nn3 = aff && P.nn3 && !P.blocks;
+    const bool mix = aff && P.nn_mix && !P.blocks;
     if (P.data_kind == CTG_DATA_U8)
         return nn3 ? launch_scan_t<LabelT, uint8_t, MODE_AFF_NN>(P, R, C, s)
+               : mix ? launch_scan_t<LabelT, uint8_t, MODE_AFF_MIX>(P, R, C, s)
                : aff ? launch_scan_t<LabelT, uint8_t, MODE_AFFINITY>(P, R, C, s)
                      : launch_scan_t<LabelT, uint8_t, MODE_BOUNDARY>(P, R, C, s);
     return nn3 ? launch_scan_t<LabelT, float, MODE_AFF_NN>(P, R, C, s)
+           : mix ? launch_scan_t<LabelT, float, MODE_AFF_MIX>(P, R, C, s)
            : aff ? launch_scan_t<LabelT, float, MODE_AFFINITY>(P, R, C, s)
                  : launch_scan_t<LabelT, float, MODE_BOUNDARY>(P, R, C, s);
 }
