@@ -263,6 +263,7 @@ def test_affinity_random_volumes(gpu, offsets):
     [[-1, 0, 0], [0, -1, 0], [0, 0, -3]],                 # one nearest-neighbour channel missing
     [[0, 0, -1], [-1, 0, 0], [0, -1, 0], [0, 0, -9]],      # nearest-neighbour channels in another order
     [[-2, 0, 0], [0, -3, 0]],                              # long-range channels only
+    [[0, 0, -1], [-1, 0, 0], [0, -1, 0]],                  # the three nearest-neighbour channels permuted
 ])
 def test_affinity_channel_sets(gpu, offsets):
     """Channel sets with and without the three nearest-neighbour offsets: the
@@ -288,6 +289,24 @@ def test_affinity_without_marker_skip_is_identical(gpu, monkeypatch):
         np.testing.assert_array_equal(a['nodes'], b['nodes'])
         np.testing.assert_array_equal(a['features'][:, 9], b['features'][:, 9])
         np.testing.assert_allclose(a['features'], b['features'], rtol=1e-12, atol=1e-12)
+
+
+@pytest.mark.parametrize('offsets', [S.NN_OFFSETS, S.LR_OFFSETS])
+def test_nearest_neighbour_faces_equal_channel_loop(gpu, monkeypatch, offsets):
+    """The face-scan forms of the affinity scan (MODE_AFF_NN for the three
+    nearest-neighbour channels, MODE_AFF_MIX beside long-range channels) give
+    the channel loop's result (CTG_NN3=0): same edges, nodes and counts,
+    features to rounding (the samples fold in another order)."""
+    lab, bnd = S.generate((20, 66, 70), cell=5, seed=23)
+    affs = S.affinities_from_boundary(bnd, offsets)
+    a = rag.rag_features(lab, affs, offsets=offsets)
+    monkeypatch.setenv('CTG_NN3', '0')
+    b = rag.rag_features(lab, affs, offsets=offsets)
+    monkeypatch.delenv('CTG_NN3')
+    np.testing.assert_array_equal(a['edges'], b['edges'])
+    np.testing.assert_array_equal(a['nodes'], b['nodes'])
+    np.testing.assert_array_equal(a['features'][:, 9], b['features'][:, 9])
+    np.testing.assert_allclose(a['features'], b['features'], rtol=1e-12, atol=1e-12)
 
 
 def test_record_regions_overflow(gpu, monkeypatch):
