@@ -291,6 +291,20 @@ def test_affinity_without_marker_skip_is_identical(gpu, monkeypatch):
         np.testing.assert_allclose(a['features'], b['features'], rtol=1e-12, atol=1e-12)
 
 
+@pytest.mark.parametrize('shape', [(1, 7, 5), (3, 1, 130), (2, 33, 1), (5, 9, 65), (7, 40, 129)])
+@pytest.mark.parametrize('offsets', [S.NN_OFFSETS, S.LR_OFFSETS])
+def test_affinity_odd_shapes(gpu, shape, offsets):
+    """Single planes, single rows / columns, ragged x tiles (65, 129 columns)
+    and y tiles (40 rows): the face-form modes and the channel loop against
+    the oracle."""
+    lab, bnd = S.generate(shape, cell=3, seed=31)
+    affs = S.affinities_from_boundary(bnd, offsets)
+    e_ref, f_ref = O.affinity_features(lab, affs, offsets)
+    out = rag.rag_features(lab, affs, offsets=offsets)
+    np.testing.assert_array_equal(out['edges'], e_ref)
+    check_features(out['features'], f_ref)
+
+
 @pytest.mark.parametrize('offsets', [S.NN_OFFSETS, S.LR_OFFSETS])
 def test_nearest_neighbour_faces_equal_channel_loop(gpu, monkeypatch, offsets):
     """The face-scan forms of the affinity scan (MODE_AFF_NN for the three
