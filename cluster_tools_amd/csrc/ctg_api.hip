@@ -423,10 +423,14 @@ static hipError_t reduce_records(Workspace& w, const ReduceJob& J, hipStream_t s
     }
     if (!O.edges || (J.stats && !O.feats)) return hipErrorOutOfMemory;
     O.count_out = may_drop ? nullptr : dE;   // no compaction: the kernel copies the count
+#ifdef CTG_DIAG   // diagnostic reduce ablations exist only in diagnostic builds (make variant EXTRA=-DCTG_DIAG)
     {
         static const int ablate = [] { const char* v = getenv("CTG_REDUCE_ABLATE"); return v ? atoi(v) : 0; }();
         O.ablate = ablate;
     }
+#else
+    O.ablate = 0;
+#endif
     e = launch_reduce(n, dE_all, w.uniq, w.runs, w.offs, packed ? nullptr : w.idx_out, packed ? w.sk_out : nullptr,
                       packed ? ib : 0, J.R, J.wide, J.stats, nb, J.umask, J.need_adj, J.ignore_label, J.scale, J.offset,
                       O, s);
