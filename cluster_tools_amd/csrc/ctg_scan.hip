@@ -619,8 +619,9 @@ __device__ __forceinline__ void fold_batch(Table& T, const StageT* __restrict__ 
             pv[i] = __hip_atomic_load(&T.w[slot[i]][24], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
 #if CTG_PAIR_FOLD
-    // grouped atomics: whole-array boundary maps
-    if constexpr (MODE == MODE_BOUNDARY && !BATCH) {
+    // grouped atomics: whole-array boundary maps and nearest-neighbour
+    // affinity faces (single-sample entries)
+    if constexpr ((MODE == MODE_BOUNDARY || MODE == MODE_AFF_NN) && !BATCH) {
         fold_grouped<MODE, FAST40, BATCH, StageT, NPER>(T, e, slot, pv, lane, R, C, scale, offset, ablate);
         return;
     }
