@@ -58,7 +58,7 @@ constexpr int ROWS_AFF = CTG_AFF_ROWS;   // affinity maps: rows per wave (the ch
 constexpr int WAVES = SCAN_THREADS / WAVE;                // 8
 constexpr int WG_ROWS = ROWS_WIDE * WAVES;                // tile y extent (the default kernel)
 #ifndef CTG_AFF_G
-#define CTG_AFF_G 3   // (2 before the nearest-neighbour channels moved to the faces: 12-channel scan 42.6 -> 42.1 ms)
+#define CTG_AFF_G 2   // (3: 12-channel scan 42.6 -> 42.1 ms, but its register spills add 26 GB of reads and 11 GB of writes)
 #endif
 // affinity channels whose gathers / sample loads / Bloom probes are issued
 // together (x ROWS rows): the channel loop is bound by memory round trips
