@@ -34,6 +34,10 @@ hipError_t bucket_runs(const uint64_t* sorted, int64_t n, int lo_bit, int hi_bit
 hipError_t bucket_sort_pairs(const uint64_t* keys, const uint32_t* vals, uint64_t* ktmp, uint32_t* vtmp,
                              uint64_t* kout, uint32_t* vout, int64_t n, int hi_bit, uint32_t* small, void** temp,
                              size_t* temp_bytes, hipStream_t s);
+hipError_t group_sort_runs(const uint64_t* key, int64_t rcap, const RegionPrefix& pre, int64_t n, int nb, int ub,
+                           int ib, uint64_t max_label, uint32_t* small, uint32_t* host_word, uint64_t* items,
+                           uint32_t* perm, uint64_t* uniq, uint32_t* runs, uint32_t* roffs, uint32_t* dE,
+                           bool* done, hipStream_t s);
 hipError_t launch_max_pairs(int64_t n, const uint64_t* uv, unsigned long long* out, hipStream_t s);
 hipError_t launch_reduce(int64_t E, const uint32_t* dE, const uint64_t* uniq, const uint32_t* runs,
                          const uint32_t* offs, const uint32_t* perm32, const uint64_t* perm64, int ib,
@@ -174,6 +178,13 @@ static hipError_t ws_init(Workspace& w) {
     if (e != hipSuccess) return e;
     e = hipMalloc(&w.bsort, BK_SMALL_WORDS * sizeof(uint32_t));   // bucket sort scratch
     if (e != hipSuccess) return e;
+    e = hipMalloc(&w.gsort, GS_SMALL_WORDS * sizeof(uint32_t));   // group sort scratch
+    if (e != hipSuccess) return e;
+    // the splitters stay in workspace memory: k_mgpu_bounds still reads them
+    // after ctg_mgpu_split returns (a pool block freed there could be handed
+    // to a call on another stream while that kernel runs)
+    e = hipMalloc(&w.mgpu_spl, CTG_MGPU_MAX_WORLD * sizeof(uint64_t));
+    if (e != hipSuccess) return e;
     e = hipHostMalloc(&w.small_host, 64 * sizeof(unsigned int), hipHostMallocDefault);
     if (e != hipSuccess) return e;
     for (int i = 0; i < 10; ++i) hipEventCreate(&w.ev[i]);
@@ -181,11 +192,16 @@ static hipError_t ws_init(Workspace& w) {
     return hipSuccess;
 }
 
-hipError_t ensure_records(Workspace& w, int64_t need, int wide) {
-    if (need <= w.rec.cap && w.rec.key) return hipSuccess;
+static void free_records(Workspace& w) {
     dfree(w.rec.key);
     dfree(w.rec.sums);
     dfree(w.rec.hist);
+    w.rec = RecordBuf{};
+}
+
+hipError_t ensure_records(Workspace& w, int64_t need, int wide) {
+    if (need <= w.rec.cap && w.rec.key) return hipSuccess;
+    free_records(w);
     const int words = wide ? WREC_WORDS : NREC_STRIDE;
     w.rec.key = (uint64_t*)dalloc((size_t)need * 8);
     w.rec.sums = wide ? (double2*)dalloc((size_t)need * 16) : nullptr;
@@ -272,13 +288,12 @@ static bool bucket_sort_pairs_on(int64_t n) {
     // the in-LDS sort of ~34 K-record buckets split into sub-buckets; profiles/r4/g)
     return n <= (int64_t)(32 << 20);
 }
-static int64_t sort_wide_digits_max() {
-    static const int64_t v = [] {
-        const char* e = getenv("CTG_SORT_WIDE_MAX");
-        return e ? (int64_t)atoll(e) : (int64_t)(64 << 20);
-    }();
-    return v;
+// CTG_GROUP_SORT=0: the (key, slot) scan records take the bucket / onesweep paths
+static bool group_sort_on() {
+    const char* e = getenv("CTG_GROUP_SORT");   // read per call: tests switch it
+    return !(e && e[0] == '0');
 }
+static int64_t sort_wide_digits_max() { return (int64_t)(64 << 20); }
 
 // ---------------------------------------------------------------------------
 // shared back half: records (n, with keys (u<<32|v) or (u,v) pairs) -> result
@@ -354,19 +369,31 @@ static hipError_t reduce_records(Workspace& w, const ReduceJob& J, hipStream_t s
     // sorted order came out wrong (tests/test_gpu_blocks.py::
     // test_blocks_independent_of_workspace_history), so one bit stays free
     const bool packed = J.keys && J.regions && sort_packed() && ub + nb + ib <= 63 && n <= sort_wide_digits_max();
-    if (J.keys && J.regions)
+    // the bucket passes need keys spread over their top bits: block-tagged keys
+    // (ctg_rag_blocks, J.ub set) put the block id there and fill a few huge
+    // buckets (configs[0] device time 3.9 -> 6.7 ms), so they keep onesweep
+    const bool spread = J.ub == 0;
+    // (key, slot) scan records: the group sort reads the record regions itself
+    // (no pack pass) and writes the run table and the slot permutation
+    bool grouped = false;
+    if (J.keys && J.regions && !packed && spread && group_sort_on()) {
+        ev.mark(2);   // (phases: the whole group sort is "sort")
+        e = group_sort_runs(J.keys, J.R.rcap, *J.regions, n, nb, ub, ib, J.max_v, w.gsort, w.small_host + 16, w.sk_out,
+                            w.idx_out, w.uniq, w.runs, w.offs, dE_all, &grouped, s);
+        if (e != hipSuccess) return e;
+        if (grouped) ev.mark(3);
+    }
+    if (grouped) {
+    } else if (J.keys && J.regions)
         e = launch_pack_regions(J.keys, J.R.rcap, *J.regions, nb, packed ? ib : 0, w.sk_in, w.idx_in, s);
     else if (J.keys) e = launch_pack_keys(n, J.keys, nb, w.sk_in, w.idx_in, s);
     else e = launch_pack_pairs(n, J.pairs, nb, w.sk_in, w.idx_in, s);
     if (e != hipSuccess) return e;
-    ev.mark(2);
-    bool have_offs = false;   // run offsets already written (bucket path)
-    bool pairs_done = false;  // pair sort + runs done by the bucket path
-    // the bucket pass needs keys spread over their top bits: block-tagged keys
-    // (ctg_rag_blocks, J.ub set) put the block id there and fill a few huge
-    // buckets (configs[0] device time 3.9 -> 6.7 ms), so they keep onesweep
-    const bool spread = J.ub == 0;
-    if (packed && spread && bucket_sort()) {
+    if (!grouped) ev.mark(2);
+    bool have_offs = grouped;     // run offsets already written (bucket / group path)
+    bool pairs_done = grouped;    // pair sort + runs done by the bucket / group path
+    if (grouped) {
+    } else if (packed && spread && bucket_sort()) {
         // MSD bucket pass + segmented sort of the key bits (ctg_sort.hip):
         // 4 fused launches instead of 4 onesweep passes with their fills
         e = bucket_sort_keys(w.sk_in, w.uniq, w.sk_out, n, ib, ib + ub + nb, w.bsort, &w.temp, &w.temp_bytes, s);
@@ -594,15 +621,8 @@ int ctg_mgpu_split(const ctg_result* local, const int64_t* meta_all, int world_s
     if (!mgpu_args(local, world_size, "ctg_mgpu_split") || !meta_all || !counts) return CTG_ERR_ARG;
     Workspace& w = ws(cur_dev());
     CTG_CHECK(ws_init(w));
-    uint64_t* spl = (uint64_t*)dalloc(CTG_MGPU_MAX_WORLD * 8);
-    if (!spl) {
-        set_error("ctg_mgpu_split: out of device memory");
-        return CTG_ERR_NOMEM;
-    }
-    const hipError_t e = mgpu_split(local->edges, local->n_edges, local->nodes, local->n_nodes, meta_all,
-                                    world_size, spl, counts, (hipStream_t)stream);
-    dfree(spl);   // stream-ordered reuse
-    CTG_CHECK(e);
+    CTG_CHECK(mgpu_split(local->edges, local->n_edges, local->nodes, local->n_nodes, meta_all, world_size,
+                         w.mgpu_spl, counts, (hipStream_t)stream));
     return CTG_OK;
 }
 
@@ -637,6 +657,10 @@ int ctg_mgpu_merge(ctg_result* local, const int64_t* recv, const int64_t* counts
         !(hist_hi > hist_lo))
         return CTG_ERR_ARG;
     *out = nullptr;
+    if (!local->owned.empty()) {   // a shard's arrays are interior pointers of its owned blocks
+        set_error("ctg_mgpu_merge: the local table is itself a merge shard; pass the rank's local call");
+        return CTG_ERR_ARG;
+    }
     int64_t rows = 0, nodes = 0, recv_words = 0;
     for (int d = 0; d < world_size; ++d) {
         rows += counts_all[((int64_t)rank * world_size + d) * 2];
@@ -657,8 +681,13 @@ int ctg_mgpu_merge(ctg_result* local, const int64_t* recv, const int64_t* counts
     CTG_CHECK(ws_init(w));
     ctg_result* r = new ctg_result();
     r->device = cur_dev();
+    int lib_rc = CTG_OK;
     const hipError_t e = mgpu_merge(local, recv, counts_all, world_size, rank, hist_lo, hist_hi,
-                                    (hipStream_t)stream, r);
+                                    (hipStream_t)stream, r, &lib_rc);
+    if (lib_rc != CTG_OK) {   // the message is set already
+        ctg_free(r);
+        return lib_rc;
+    }
     if (e != hipSuccess) {
         set_error(std::string("ctg_mgpu_merge: ") + hipGetErrorString(e));
         ctg_free(r);
@@ -695,8 +724,7 @@ int ctg_trim(void) {
     const int d = cur_dev();
     Workspace& w = ws(d);
     CTG_CHECK(hipDeviceSynchronize());
-    dfree(w.rec.key); dfree(w.rec.sums); dfree(w.rec.hist);
-    w.rec = RecordBuf{};
+    free_records(w);
     dfree(w.sk_in); dfree(w.sk_out); dfree(w.idx_in); dfree(w.idx_out);
     dfree(w.uniq); dfree(w.runs); dfree(w.offs); dfree(w.keep); dfree(w.pos);
     w.sk_in = w.sk_out = w.uniq = nullptr;
@@ -854,8 +882,7 @@ static int scan_records(Workspace& w, const ScanParams& P, int64_t V, hipStream_
     *overflow = false;
     if (getenv("CTG_REC_FRESH")) {   // test hook: start from the smallest record buffer
         CTG_CHECK(hipStreamSynchronize(s));
-        dfree(w.rec.key); dfree(w.rec.sums); dfree(w.rec.hist);
-        w.rec = RecordBuf{};
+        free_records(w);
     }
     int64_t need = std::max<int64_t>(w.rec.cap, std::max<int64_t>(1 << 16, V / 24));
     need = (need + NREG - 1) / NREG * NREG;
@@ -963,7 +990,6 @@ int ctg_rag_features(const void* labels, int label_bits, const void* data, int d
     // flush decisions every check_planes planes (overflow safety does not
     // depend on it: ctg_scan.hip's per-wave sample budget bounds every count)
     P.check_planes = 8;
-    if (const char* cp = getenv("CTG_CHECK_PLANES")) P.check_planes = std::max(1, atoi(cp));
     // planes per workgroup of the narrow-tile launch (fragmented volumes):
     // shallower tiles split fewer edges at table flushes (profiles/r4/tz)
     constexpr int NARROW_TILE_Z = 16;
@@ -992,18 +1018,16 @@ int ctg_rag_features(const void* labels, int label_bits, const void* data, int d
             while (tzn < tz && cols_n * ((shape[0] + tzn - 1) / tzn) > 65536) tzn *= 2;
             P.tile_z_narrow = tzn;
         }
-        if (const char* t = getenv("CTG_TILE_Z")) P.tile_z_narrow = tz = std::max(1, atoi(t));
-        if (const char* t = getenv("CTG_TILE_Z_NARROW")) P.tile_z_narrow = std::max(1, atoi(t));
+        if (const char* t = getenv("CTG_TILE_Z")) P.tile_z_narrow = tz = std::max(1, atoi(t));   // tests
         P.tile_z = tz;
     }
+#ifdef CTG_DIAG   // scan ablations (variant builds only)
     {
         const char* ab = getenv("CTG_ABLATE");
         P.ablate = ab ? atoi(ab) : 0;
     }
-    {
-        const char* xr = getenv("CTG_XCD_REMAP");
-        P.xcd_remap = xr ? atoi(xr) : 1;
-    }
+#endif
+    P.xcd_remap = 1;
     // boundary maps of fragmented volumes (configs[4]: cell 5) scan with
     // 2-row waves: the sampled x-face density decides on the device (cell 10
     // ~ 0.10, cell 5 ~ 0.20 changes per pair; threshold 0.14), without a host
@@ -1051,8 +1075,7 @@ int ctg_rag_features(const void* labels, int label_bits, const void* data, int d
             // load per long-range sample (vs. a probe chain in a set 4x the
             // size); the reduce drops its false positives (keys no
             // nearest-neighbour sample flagged)
-            const char* bpk = getenv("CTG_BLOOM_BPK");   // A/B: bits per edge
-            const int64_t bits = adj_graph->n_edges * (bpk ? std::max(1, atoi(bpk)) : 48);
+            const int64_t bits = adj_graph->n_edges * 48;
             uint32_t blocks = 128;   // 64-B blocks
             while ((int64_t)blocks * 512 < bits) blocks *= 2;
             bloom = (unsigned long long*)dalloc((size_t)blocks * 64);

@@ -120,7 +120,7 @@ struct RegionPrefix {          // exclusive prefix of the region counts (host-co
 
 struct RecordBuf {
     uint64_t* key = nullptr;      // (u << 32) | v
-    double2* sums = nullptr;      // wide records: (sum, sum of squares); narrow: unused (in the body)
+    double2* sums = nullptr;      // wide records: (sum, sum of squares); compact: unused (in the body)
     uint32_t* hist = nullptr;     // narrow: NREC_STRIDE-word bodies; wide: WREC_WORDS per record
     int64_t cap = 0;
     int64_t rcap = 0;             // slots per region (cap / NREG)
@@ -213,6 +213,7 @@ struct ReduceOut {
 };
 
 constexpr int BK_SMALL_WORDS = 5 * 4096 + 16;   // bucket sort: counts, offsets, cursors, run heads
+constexpr int GS_SMALL_WORDS = 5 * 65536 + 8;    // group sort: counts, offsets, cursors, misc, look-back state
 
 struct Workspace {
     int device = -1;
@@ -230,6 +231,8 @@ struct Workspace {
     unsigned int* small = nullptr;       // device scalars (run counts etc.)
     unsigned int* small_host = nullptr;
     uint32_t* bsort = nullptr;           // device: bucket-sort scratch, BK_SMALL_WORDS u32 (ctg_sort.hip)
+    uint32_t* gsort = nullptr;           // device: group-sort scratch, GS_SMALL_WORDS u32 (ctg_sort.hip)
+    uint64_t* mgpu_spl = nullptr;        // device: the exchange's splitters, CTG_MGPU_MAX_WORLD u64
     // host->device staging of volumes
     void* stage[2] = {nullptr, nullptr};
     size_t stage_bytes[2] = {0, 0};
@@ -283,8 +286,10 @@ hipError_t mgpu_split(const uint64_t* edges, int64_t E, const uint64_t* nodes, i
                       int world, uint64_t* spl, int64_t* counts, hipStream_t s);
 hipError_t mgpu_pack(const ctg_result* r, const int64_t* counts_all, int world, int rank, int64_t* send,
                      hipStream_t s);
+// *lib_rc: a library status (with its message set) when a nested C-ABI call
+// failed, or CTG_ERR_UNSUPPORTED for a shard past the u32 row indices
 hipError_t mgpu_merge(ctg_result* local, const int64_t* recv, const int64_t* counts_all, int world, int rank,
-                      double hist_lo, double hist_hi, hipStream_t s, ctg_result* out);
+                      double hist_lo, double hist_hi, hipStream_t s, ctg_result* out, int* lib_rc);
 }  // namespace ctg
 
 #define CTG_CHECK(expr)                                                        \

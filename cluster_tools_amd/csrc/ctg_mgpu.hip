@@ -460,8 +460,9 @@ static unsigned grid_of(int64_t n) { return (unsigned)std::max<int64_t>((n + 255
 
 // ctg_mgpu_merge (include/ctg.h): this rank's shard of the global table.
 hipError_t mgpu_merge(ctg_result* L, const int64_t* recv, const int64_t* counts_all, int world, int rank,
-                      double hist_lo, double hist_hi, hipStream_t s, ctg_result* r) {
+                      double hist_lo, double hist_hi, hipStream_t s, ctg_result* r, int* lib_rc) {
     Workspace& w = ws(r->device);
+    *lib_rc = CTG_OK;
     // own range: rows / node ids this rank kept for itself
     const int64_t* mine = counts_all + (int64_t)rank * world * 2;
     int64_t e_lo = 0, n_lo = 0;
@@ -525,7 +526,10 @@ hipError_t mgpu_merge(ctg_result* L, const int64_t* recv, const int64_t* counts_
         if ((e = hipGetLastError()) != hipSuccess) return e;
         ctg_result* U = nullptr;
         const int rc = ctg_unique_values(list, total, CTG_MEM_DEVICE, s, &U);
-        if (rc) return hipErrorUnknown;
+        if (rc) {   // its status and message pass through
+            *lib_rc = rc;
+            return hipErrorUnknown;
+        }
         r->nodes = U->nodes;
         r->n_nodes = U->n_nodes;
         r->owned.push_back(U->nodes);
@@ -545,6 +549,12 @@ hipError_t mgpu_merge(ctg_result* L, const int64_t* recv, const int64_t* counts_
         return hipSuccess;
     }
     if (!L->stats || !L->features) return hipErrorInvalidValue;   // needs a CTG_KEEP_STATS partial table
+    // row indices, run heads and output positions below are u32
+    if (M >= (1ll << 32) || e_cnt + M >= (1ll << 32) || NM >= (1ll << 32)) {
+        set_error("ctg_mgpu_merge: more than 2^32 rows in one shard (split the slab over more ranks)");
+        *lib_rc = CTG_ERR_UNSUPPORTED;
+        return hipErrorNotSupported;
+    }
     MergeIO io{};
     io.own_edges = L->edges + 2 * e_lo;
     io.own_feats = L->features + 10 * e_lo;

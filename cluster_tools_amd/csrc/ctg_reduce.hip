@@ -149,6 +149,7 @@ __device__ __forceinline__ void reduce_epilogue(int64_t e, uint64_t u, uint32_t 
     }
     if (!O.feats) return;
     double* o = O.feats + (size_t)e * N_FEATURES;
+#ifdef CTG_DIAG
     if (O.ablate & 4) {   // keep the values live without the 80-B row stores
         double t = sum + sq + (double)cnt + (double)mn + (double)mx;
 #pragma unroll
@@ -157,6 +158,9 @@ __device__ __forceinline__ void reduce_epilogue(int64_t e, uint64_t u, uint32_t 
         return;
     }
     finalize_row(h, cnt, mn, mx, mo, scale, offset, o, !(O.ablate & 1));
+#else
+    finalize_row(h, cnt, mn, mx, mo, scale, offset, o);
+#endif
 }
 
 template <bool WIDE, bool STATS>
@@ -194,16 +198,16 @@ __global__ __launch_bounds__(256) void k_reduce_edges(int64_t E, const uint32_t*
         uint32_t cnt = 0, mn = ORD_POS_INF, mx = ORD_NEG_INF;
         Moments mo;
         const uint32_t b = offs[e], n = runs[e];
+#ifdef CTG_DIAG   // diagnostic ablation (CTG_REDUCE_ABLATE, variant builds only)
         if (O.ablate & 2) {
             cnt = n;
             h[1] = n;
             mn = mx = 0x3F800000u ^ 0x80000000u;
             mo.add(n, 0.0, 0.0, 0u);
-        } else {
-            for (uint32_t r = b; r < b + n; ++r) {
-                const uint32_t i = perm(r);
-                load_record<WIDE>(R, i, h, cnt, flags, mn, mx, mo);
-            }
+        } else
+#endif
+        {
+            for (uint32_t r = b; r < b + n; ++r) load_record<WIDE>(R, perm(r), h, cnt, flags, mn, mx, mo);
         }
         reduce_epilogue(e, u, h, cnt, flags, mn, mx, mo, umask, need_adj, ignore_label, scale, offset, O);
     }
@@ -240,18 +244,6 @@ __global__ void k_endpoints(int64_t E, const uint64_t* __restrict__ uniq, int nb
     out[2 * e + 1] = (uint32_t)(sk & ((1ull << nb) - 1ull));
 }
 
-// nodes as a bitmap over [0, max label]: u is sorted in the key table, so only
-// run heads mark it; every v marks its bit
-__global__ void k_mark_nodes(int64_t E, const uint32_t* __restrict__ dE, const uint64_t* __restrict__ uniq, int nb,
-                             uint32_t* __restrict__ bits) {
-    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (e >= E || e >= (int64_t)*dE) return;
-    const uint64_t sk = uniq[e];
-    const uint32_t u = (uint32_t)(sk >> nb), v = (uint32_t)(sk & ((1ull << nb) - 1ull));
-    if (e == 0 || (uint32_t)(uniq[e - 1] >> nb) != u) atomicOr(&bits[u >> 5], 1u << (u & 31));
-    atomicOr(&bits[v >> 5], 1u << (v & 31));
-}
-
 __global__ void k_bits_to_nodes(int64_t W, const uint32_t* __restrict__ bits, const uint32_t* __restrict__ off,
                                 uint64_t* __restrict__ nodes, uint32_t* __restrict__ dN) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -266,7 +258,9 @@ __global__ void k_bits_to_nodes(int64_t W, const uint32_t* __restrict__ bits, co
     }
 }
 
-// Same bitmap, built per chunk of the sorted key table in LDS.  A chunk of
+// Nodes as a bitmap over [0, max label], built per chunk of the sorted key
+// table in LDS (u is sorted, so only run heads mark it; every v marks its
+// bit).  A chunk of
 // NODE_CHUNK consecutive edges covers a narrow u range and, for spatially
 // ordered label ids, a narrow v window above it: the workgroup marks its
 // nodes in an LDS window and ORs the non-zero words into the global bitmap
@@ -321,10 +315,7 @@ __global__ __launch_bounds__(256) void k_mark_nodes_win(int64_t E, const uint32_
 hipError_t launch_mark_nodes(int64_t E, const uint32_t* dE, const uint64_t* uniq, int nb, uint32_t* bits,
                              hipStream_t s) {
     if (E == 0) return hipSuccess;
-    if (getenv("CTG_NODES_ATOMIC"))   // A/B: one global atomic per edge
-        hipLaunchKernelGGL(k_mark_nodes, dim3((unsigned)((E + 255) / 256)), dim3(256), 0, s, E, dE, uniq, nb, bits);
-    else
-        hipLaunchKernelGGL(k_mark_nodes_win, dim3((unsigned)((E + NODE_CHUNK - 1) / NODE_CHUNK)), dim3(256), 0, s,
+    hipLaunchKernelGGL(k_mark_nodes_win, dim3((unsigned)((E + NODE_CHUNK - 1) / NODE_CHUNK)), dim3(256), 0, s,
                            E, dE, uniq, nb, bits);
     return hipGetLastError();
 }

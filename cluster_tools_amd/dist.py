@@ -355,5 +355,56 @@ def gather_to_host(res, root=0, group=None):
             torch.cat(nodes).numpy().view(np.uint64))
 
 
+def write_global(res, graph_path, graph_key='graph', features_path=None, features_key='features', shape=None,
+                 ignore_label=False, root=0, group=None, n_threads=8, timings=None):
+    """SURVEY §8(e) Output: gather the shards on ``root`` (gather_to_host) and
+    write what MergeSubGraphs / MergeEdgeFeatures write for the same volume:
+
+    * ``graph_path/graph_key/{nodes,edges}`` (chunks min(262144, N) / (min(262144,
+      E), 2), gzip) with attrs numberOfNodes / numberOfEdges
+      (merge_sub_graphs.py:127-137, ndist.mergeSubgraphs), ``shape``
+      (:137) and ``ignore_label`` (graph_workflow.py's sub-graph attrs, :63-68);
+    * ``features_path/features_key`` (E, 10) float64, chunks (min(262144, E), 1),
+      gzip (merge_edge_features.py:62-65, written per edge range at :141-147).
+
+    Collective; the N5 write happens on ``root`` only (returns (E, N) there,
+    None elsewhere).  ``timings`` (dict) receives 'gather_s' and 'write_s'."""
+    from . import n5
+    t0 = time.perf_counter()
+    got = gather_to_host(res, root=root, group=group)
+    t1 = time.perf_counter()
+    if timings is not None:
+        timings['gather_s'] = t1 - t0
+    if got is None:
+        return None
+    edges, feats, nodes = got
+    n_edges, n_nodes = int(edges.shape[0]), int(nodes.shape[0])
+    with n5.file_reader(graph_path) as f:
+        g = f.require_group(graph_key)
+        ds_n = g.require_dataset('nodes', shape=(n_nodes,), chunks=(max(1, min(n_nodes, 262144)),),
+                                 dtype='uint64', compression='gzip')
+        ds_e = g.require_dataset('edges', shape=(n_edges, 2), chunks=(max(1, min(n_edges, 262144)), 2),
+                                 dtype='uint64', compression='gzip')
+        ds_n.n_threads = ds_e.n_threads = max(1, int(n_threads))
+        if n_nodes:
+            ds_n[:] = nodes
+        if n_edges:
+            ds_e[:] = edges
+        g.attrs['numberOfNodes'] = n_nodes
+        g.attrs['numberOfEdges'] = n_edges
+        if shape is not None:
+            g.attrs['shape'] = [int(v) for v in shape]
+        g.attrs['ignore_label'] = bool(ignore_label)
+    with n5.file_reader(features_path or graph_path) as f:
+        ds_f = f.require_dataset(features_key, shape=(n_edges, 10), chunks=(max(1, min(n_edges, 262144)), 1),
+                                 dtype='float64', compression='gzip')
+        ds_f.n_threads = max(1, int(n_threads))
+        if n_edges:
+            ds_f[:] = feats
+    if timings is not None:
+        timings['write_s'] = time.perf_counter() - t1
+    return n_edges, n_nodes
+
+
 def world_size_of(group):
     return dist.get_world_size(group) if dist.is_initialized() else 1

@@ -260,3 +260,63 @@ def test_mgpu_slab_plan_c_abi():
         cdist.slab_plan(4, 8, 0)
     with pytest.raises(_lib.CtgError):
         cdist.slab_plan(64, 2, 2)
+
+
+def _gather_worker(rank, world, port, shape, cell, outdir, big):
+    import torch.distributed as dist
+    from tests.dist_helpers import OracleBackend
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    lab, bnd = _volume(shape, cell, big)
+    Z = shape[0]
+    z0 = [Z * r // world for r in range(world + 1)]
+    halo = 1 if rank > 0 else 0
+    sl = slice(z0[rank] - halo, z0[rank + 1])
+    res = cdist.rag_features_distributed(np.ascontiguousarray(lab[sl]), np.ascontiguousarray(bnd[sl]),
+                                         own_begin=(halo, 0, 0), backend=OracleBackend())
+    root = world - 1   # not rank 0: the root argument is honoured
+    got = cdist.gather_to_host(res, root=root)
+    assert (got is None) == (rank != root)
+    if got is not None:
+        e, f, n = got
+        np.save(os.path.join(outdir, 'ge.npy'), e)
+        np.save(os.path.join(outdir, 'gf.npy'), f)
+        np.save(os.path.join(outdir, 'gn.npy'), n)
+    t = {}
+    w = cdist.write_global(res, os.path.join(outdir, 'out.n5'), 'graph', os.path.join(outdir, 'feat.n5'),
+                           'features', shape=shape, ignore_label=False, root=0, timings=t)
+    assert (w is None) == (rank != 0) and 'gather_s' in t
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize('world,shape,cell,big', [
+    (2, (24, 40, 36), 6, False),
+    (3, (30, 33, 29), 5, 'huge'),
+    (4, (32, 24, 20), 5, 'flat_top'),   # the upper ranks' shards are empty
+])
+def test_gather_to_host_and_n5_write(tmp_path, world, shape, cell, big):
+    """SURVEY §8(e) Output: gather_to_host puts the global tables on the root
+    (any rank), and write_global writes graph/{nodes,edges} with the
+    MergeSubGraphs attrs and the (E, 10) features dataset with
+    merge_edge_features.py's chunks; both equal the whole-volume oracle."""
+    mp.spawn(_gather_worker, args=(world, _free_port(), shape, cell, str(tmp_path), big), nprocs=world, join=True)
+    lab, bnd = _volume(shape, cell, big)
+    e_ref, f_ref = O.boundary_features(lab, bnd)
+    nodes_ref = O.unique_labels(O.rag_edges(lab))
+    e = np.load(tmp_path / 'ge.npy')
+    np.testing.assert_array_equal(e, e_ref)
+    np.testing.assert_allclose(np.load(tmp_path / 'gf.npy'), f_ref, rtol=1e-9, atol=1e-12)
+    np.testing.assert_array_equal(np.load(tmp_path / 'gn.npy'), nodes_ref)
+    from cluster_tools_amd import n5
+    with n5.file_reader(str(tmp_path / 'out.n5'), 'r') as f:
+        g = f['graph']
+        assert g.attrs['numberOfEdges'] == e_ref.shape[0] and g.attrs['numberOfNodes'] == nodes_ref.shape[0]
+        assert list(g.attrs['shape']) == list(shape) and g.attrs['ignore_label'] is False
+        assert tuple(g['edges'].chunks) == (min(262144, e_ref.shape[0]), 2)
+        np.testing.assert_array_equal(g['edges'][:], e_ref)
+        np.testing.assert_array_equal(g['nodes'][:], nodes_ref)
+    with n5.file_reader(str(tmp_path / 'feat.n5'), 'r') as f:
+        ds = f['features']
+        assert tuple(ds.shape) == (e_ref.shape[0], 10) and tuple(ds.chunks) == (min(262144, e_ref.shape[0]), 1)
+        np.testing.assert_allclose(ds[:], f_ref, rtol=1e-9, atol=1e-12)

@@ -97,6 +97,14 @@ def _rccl_worker(rank, world, port, outdir, affinity):
     calls_reads = list(cdist.host_reads)
     assert res.edge_offset == 0 and res.n_edges_global == res.n_edges   # the lazy shard-size read
     np.save(os.path.join(outdir, 'reads.npy'), np.array(calls_reads + list(cdist.host_reads)))
+    # SURVEY §8(e) Output over RCCL: the shards gathered in HBM on the root, then the N5 write
+    e, f, n = cdist.gather_to_host(res, root=0)
+    np.save(os.path.join(outdir, 'ge.npy'), e)
+    np.save(os.path.join(outdir, 'gf.npy'), f)
+    np.save(os.path.join(outdir, 'gn.npy'), n)
+    t = {}
+    assert cdist.write_global(res, os.path.join(outdir, 'out.n5'), shape=SHAPE, timings=t) == (len(e), len(n))
+    assert t['gather_s'] >= 0 and t['write_s'] >= 0
     dist.destroy_process_group()
 
 
@@ -115,6 +123,15 @@ def test_rccl_world1_exchange_equals_single_call(tmp_path, affinity):
     np.testing.assert_array_equal(np.load(tmp_path / 'n.npy').astype(np.uint64), ref['nodes'])
     # one count-matrix read per call; the shard sizes when first asked for
     assert list(np.load(tmp_path / 'reads.npy')) == ['counts', 'counts', 'offsets']
+    np.testing.assert_array_equal(np.load(tmp_path / 'ge.npy'), ref['edges'])
+    np.testing.assert_allclose(np.load(tmp_path / 'gf.npy'), ref['features'], rtol=1e-9, atol=1e-12)
+    np.testing.assert_array_equal(np.load(tmp_path / 'gn.npy'), ref['nodes'])
+    from cluster_tools_amd import n5
+    with n5.file_reader(str(tmp_path / 'out.n5'), 'r') as fh:
+        np.testing.assert_array_equal(fh['graph/edges'][:], ref['edges'])
+        np.testing.assert_array_equal(fh['graph/nodes'][:], ref['nodes'])
+        assert fh['graph'].attrs['numberOfEdges'] == ref['edges'].shape[0]
+        np.testing.assert_allclose(fh['features'][:], ref['features'], rtol=1e-9, atol=1e-12)
 
 
 @pytest.mark.parametrize('affinity', [False, True, 'lr'])

@@ -539,45 +539,100 @@ def test_bucket_sort_skewed_keys(gpu, monkeypatch):
     check_features(out['features'], f_o)
 
 
-@pytest.mark.parametrize('packed', ['1', '0'])
-@pytest.mark.parametrize('shape,cell', [((48, 96, 130), 5), ((64, 128, 128), 3)])
-def test_lds_bucket_sort_matches_segmented(gpu, monkeypatch, packed, shape, cell):
-    """The in-LDS bucket sort (ctg_sort.hip k_bucket_lds_sort: one workgroup
-    per MSD bucket, sub-buckets above the LDS capacity) against rocPRIM's
-    segmented sort of the same buckets (CTG_LDS_SORT=0), on packed record keys
-    and on (key, slot) pairs (CTG_SORT_PACKED=0): same edges, counts, min /
-    max, features to the last bits of the record summation order -- and the
-    oracle."""
-    lab, bnd = S.generate(shape, cell=cell, seed=11)
-    monkeypatch.setenv('CTG_SORT_PACKED', packed)
-    monkeypatch.setenv('CTG_BUCKET_SORT_PAIRS', '1')
-    monkeypatch.setenv('CTG_LDS_SORT', '1')
-    out = rag.rag_features(lab, bnd)
-    monkeypatch.setenv('CTG_LDS_SORT', '0')
-    ref = rag.rag_features(lab, bnd)
+def _same_result(out, ref, exact_sums=False):
     np.testing.assert_array_equal(out['edges'], ref['edges'])
     np.testing.assert_array_equal(out['nodes'], ref['nodes'])
     np.testing.assert_array_equal(out['features'][:, [2, 8, 9]], ref['features'][:, [2, 8, 9]])
     np.testing.assert_allclose(out['features'], ref['features'], rtol=1e-12, atol=1e-15)
+
+
+@pytest.mark.parametrize('shape,cell,seed', [((48, 96, 130), 5, 11), ((64, 128, 128), 3, 12), ((9, 70, 300), 7, 13)])
+def test_group_sort_matches_other_paths(gpu, monkeypatch, shape, cell, seed):
+    """The group sort of (key, slot) records (ctg_sort.hip k_gs_*: bucket
+    passes over the record regions, per-bucket LDS counting sort + in-group
+    ranks, decoupled look-back for the run index) against the onesweep pair
+    sort (CTG_GROUP_SORT=0, CTG_BUCKET_SORT_PAIRS=0) and the oracle."""
+    lab, bnd = S.generate(shape, cell=cell, seed=seed)
+    monkeypatch.setenv('CTG_SORT_PACKED', '0')   # small volumes would pack key + slot into one word
+    out = rag.rag_features(lab, bnd)
+    monkeypatch.setenv('CTG_GROUP_SORT', '0')
+    monkeypatch.setenv('CTG_BUCKET_SORT_PAIRS', '0')
+    ref = rag.rag_features(lab, bnd)
+    _same_result(out, ref)
     e_o, f_o = O.boundary_features(lab, bnd)
     np.testing.assert_array_equal(out['edges'], e_o)
     check_features(out['features'], f_o)
 
 
-def test_lds_bucket_sort_skew_falls_back(gpu, monkeypatch):
-    """One edge with more records than a workgroup sorts in LDS: two planes
-    of two labels over 4096 x 4096 (one (1, 2) record per 64 x 32 tile, 8192
-    of them in one bucket).  The in-LDS sort flags the bucket and the
-    segmented sort redoes the pass: one edge, every face counted."""
+def test_group_sort_one_label_group(gpu, monkeypatch):
+    """Every record of one bucket in one in-bucket group (label 1 under a
+    plane of ~10 K cells: keys (1, v) only differ in v), and labels >= 2^20 so
+    the group bits are u's: the in-group rank pass over a ~10 K-item group."""
+    lab2, bnd2 = S.generate((1, 512, 512), cell=5, seed=3)
+    lab = np.empty((2, 512, 512), np.uint64)
+    lab[0] = 1
+    lab[1] = lab2[0] + np.uint64(1 << 20)
+    bnd = np.concatenate([np.full((1, 512, 512), 0.3, np.float32), bnd2])
+    monkeypatch.setenv('CTG_SORT_PACKED', '0')
+    out = rag.rag_features(lab, bnd)
+    monkeypatch.setenv('CTG_GROUP_SORT', '0')
+    monkeypatch.setenv('CTG_BUCKET_SORT_PAIRS', '0')
+    ref = rag.rag_features(lab, bnd)
+    _same_result(out, ref)
+    e_o, f_o = O.boundary_features(lab, bnd)
+    np.testing.assert_array_equal(out['edges'], e_o)
+    check_features(out['features'], f_o)
+
+
+def test_group_sort_oversized_bucket_falls_back(gpu, monkeypatch):
+    """Background label 1 on every other plane of a 64 x 1024 x 1024 volume:
+    the (1, v) records of ~250 K cells crowd one bucket far past the LDS
+    capacity, so the host takes the onesweep path; same result as forcing it."""
+    lab, bnd = S.generate((64, 1024, 1024), cell=6, seed=5)
+    lab = lab + np.uint64(1)
+    lab[::2] = 1
+    monkeypatch.setenv('CTG_SORT_PACKED', '0')
+    out = rag.rag_features(lab, bnd)
+    monkeypatch.setenv('CTG_GROUP_SORT', '0')
+    monkeypatch.setenv('CTG_BUCKET_SORT_PAIRS', '0')
+    ref = rag.rag_features(lab, bnd)
+    _same_result(out, ref)
+    assert np.all(out['edges'][:, 0][out['edges'][:, 1] > 1] >= 1)
+
+
+@pytest.mark.parametrize('shape,cell,quant', [((40, 80, 96), 5, None), ((48, 64, 128), 4, 4), ((32, 96, 70), 9, 2),
+                                              ((24, 130, 200), 3, None)])
+def test_narrow_tile_matches_wide_tile(gpu, monkeypatch, shape, cell, quant):
+    """The narrow-tile scan (CTG_NARROW_ROWS=1: 2-row waves, 16-plane tiles,
+    one staged entry per lane -- the configs[4] kernel, otherwise only reached
+    at 1024^3) against the wide-tile scan and the oracle, on small volumes.
+    quant: the boundary map rounded to that many levels (histogram slots
+    with many samples)."""
+    lab, bnd = S.generate(shape, cell=cell, seed=21)
+    if quant:
+        bnd = (np.round(bnd * quant) / quant).astype(np.float32)
+    monkeypatch.setenv('CTG_NARROW_ROWS', '1')
+    out = rag.rag_features(lab, bnd)
+    monkeypatch.setenv('CTG_NARROW_ROWS', '0')
+    ref = rag.rag_features(lab, bnd)
+    _same_result(out, ref)
+    e_o, f_o = O.boundary_features(lab, bnd)
+    np.testing.assert_array_equal(out['edges'], e_o)
+    check_features(out['features'], f_o)
+
+
+def test_single_edge_many_records(gpu, monkeypatch):
+    """One edge with a record from every tile: two planes of two labels over
+    4096 x 4096 (8192 (1, 2) records, all in one bucket and one in-bucket
+    group of the group sort; packed keys take the bucket sort).  One edge,
+    every face counted, exact statistics."""
     lab = np.ones((2, 4096, 4096), np.uint64)
     lab[1] = 2
     bnd = np.zeros(lab.shape, np.float32)
     bnd[0] = 0.25
     bnd[1] = 0.75
-    monkeypatch.setenv('CTG_LDS_SORT', '1')
     for packed in ('1', '0'):
         monkeypatch.setenv('CTG_SORT_PACKED', packed)
-        monkeypatch.setenv('CTG_BUCKET_SORT_PAIRS', '1')
         out = rag.rag_features(lab, bnd)
         assert out['edges'].tolist() == [[1, 2]]
         f = out['features'][0]

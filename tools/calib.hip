@@ -1,0 +1,149 @@
+// Counter calibration for the access widths the path uses.
+//
+// Each kernel moves an exactly known number of bytes with one access shape:
+//   rd16 / rd8 / rd4   streaming reads, 16 / 8 / 4 B per lane (16-B: the guide's
+//                      calibrated case; 8 B: the scan's u64 label loads; 4 B: its
+//                      f32 sample loads and the long-range 4-B label gathers)
+//   rd12               the scan's label + sample pair: 8 B and 4 B per lane from
+//                      two arrays in one pass
+//   wr16 / wr8         streaming stores, 16 / 8 B per lane (record bodies / keys)
+//   g128 / g64         random whole-record gathers, one lane per record reading
+//                      8 / 4 16-B pieces (the reduce's 128-B bodies / a 64-B body)
+//   gl8 / gl4          the same records, 8 / 4 lanes per record, 16 B each
+//   s8                 8-B stores to a random permutation of slots (bucket scatter)
+// Run it under rocprofv3 --kernel-trace and under separate --pmc FETCH_SIZE /
+// WRITE_SIZE passes; tools/calib_summary.py divides the algorithmic bytes by the
+// counters per kernel.
+//   build: hipcc -O3 --offload-arch=gfx950 tools/calib.hip -o tools/calib
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+
+#define CK(x)                                                                      \
+    do {                                                                           \
+        hipError_t e_ = (x);                                                       \
+        if (e_ != hipSuccess) {                                                    \
+            fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e_));                \
+            exit(1);                                                               \
+        }                                                                          \
+    } while (0)
+
+// a bijection of [0, 2^k): odd multiplies and xor-shifts mod 2^k
+__device__ __forceinline__ uint32_t perm_k(uint32_t x, int k) {
+    const uint32_t m = k >= 32 ? 0xFFFFFFFFu : ((1u << k) - 1u);
+    x = (x * 0x9E3779B1u) & m;
+    x ^= x >> (k / 2);
+    x = (x * 0x85EBCA6Bu) & m;
+    x ^= x >> (k / 2 + 1);
+    x = (x * 0xC2B2AE35u) & m;
+    return x;
+}
+
+template <typename T>
+__device__ __forceinline__ uint32_t fold(T v) {
+    if constexpr (sizeof(T) == 16) {
+        const uint4 u = *reinterpret_cast<const uint4*>(&v);
+        return u.x ^ u.y ^ u.z ^ u.w;
+    } else if constexpr (sizeof(T) == 8) {
+        return (uint32_t)v ^ (uint32_t)(v >> 32);
+    } else {
+        return (uint32_t)v;
+    }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_rd(const T* __restrict__ p, size_t n, uint32_t* out) {
+    uint32_t acc = 0;
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) acc ^= fold(p[i]);
+    if (acc == 0x12345678u) out[0] = acc;   // keeps the loads; never true for the zero-filled input
+}
+
+__global__ __launch_bounds__(256) void k_rd12(const uint64_t* __restrict__ a, const float* __restrict__ b, size_t n,
+                                              uint32_t* out) {
+    uint32_t acc = 0;
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256)
+        acc ^= (uint32_t)a[i] ^ __float_as_uint(b[i]);
+    if (acc == 0x12345678u) out[0] = acc;
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_wr(T* __restrict__ p, size_t n) {
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
+        T v;
+        __builtin_memset(&v, (int)(i & 0x7F), sizeof(T));
+        p[i] = v;
+    }
+}
+
+// one lane per record: PIECES 16-B loads of record perm(i)
+template <int PIECES>
+__global__ __launch_bounds__(256) void k_gather(const uint4* __restrict__ rec, int k, uint32_t n, uint32_t* out) {
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const uint4* r = rec + (size_t)perm_k(i, k) * PIECES;
+    uint32_t acc = 0;
+#pragma unroll
+    for (int j = 0; j < PIECES; ++j) acc ^= fold(r[j]);
+    if (acc == 0x12345678u) out[0] = acc;
+}
+
+// PIECES lanes per record, one 16-B piece each (the flush / a lane-group reduce)
+template <int PIECES>
+__global__ __launch_bounds__(256) void k_gather_lanes(const uint4* __restrict__ rec, int k, uint32_t n, uint32_t* out) {
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n * PIECES) return;
+    const uint4 v = rec[(size_t)perm_k(i / PIECES, k) * PIECES + (i % PIECES)];
+    if (fold(v) == 0x12345678u) out[0] = 1u;
+}
+
+__global__ __launch_bounds__(256) void k_scatter8(uint64_t* __restrict__ p, int k, uint32_t n) {
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i < n) p[perm_k(i, k)] = (uint64_t)i;
+}
+
+int main(int argc, char** argv) {
+    const int reps = argc > 1 ? atoi(argv[1]) : 3;
+    const size_t bytes = 1ull << 32;   // 4 GiB per stream: far past the 256 MiB Infinity Cache
+    void *a = nullptr, *b = nullptr;
+    uint32_t* out = nullptr;
+    CK(hipMalloc(&a, bytes));
+    CK(hipMalloc(&b, bytes));
+    CK(hipMalloc(&out, 64));
+    CK(hipMemset(a, 0, bytes));
+    CK(hipMemset(b, 0, bytes));
+    const int grid = 256 * 32;
+    printf("{\"bytes\": %zu, \"reps\": %d, \"kernels\": {", bytes, reps);
+    for (int r = 0; r < reps; ++r) {
+        hipLaunchKernelGGL(k_rd<uint4>, dim3(grid), dim3(256), 0, 0, (const uint4*)a, bytes / 16, out);
+        hipLaunchKernelGGL(k_rd<uint64_t>, dim3(grid), dim3(256), 0, 0, (const uint64_t*)a, bytes / 8, out);
+        hipLaunchKernelGGL(k_rd<uint32_t>, dim3(grid), dim3(256), 0, 0, (const uint32_t*)a, bytes / 4, out);
+        // label + sample stream: 8 B of a and 4 B of b per element (n = 2^28: 2 GiB + 1 GiB)
+        hipLaunchKernelGGL(k_rd12, dim3(grid), dim3(256), 0, 0, (const uint64_t*)a, (const float*)b,
+                           (size_t)1 << 28, out);
+        hipLaunchKernelGGL(k_wr<uint4>, dim3(grid), dim3(256), 0, 0, (uint4*)b, bytes / 16);
+        hipLaunchKernelGGL(k_wr<uint64_t>, dim3(grid), dim3(256), 0, 0, (uint64_t*)b, bytes / 8);
+        // 2^25 records of 128 B (4 GiB) / 2^26 records of 64 B (4 GiB), each read once
+        hipLaunchKernelGGL(k_gather<8>, dim3((1u << 25) / 256), dim3(256), 0, 0, (const uint4*)a, 25, 1u << 25, out);
+        hipLaunchKernelGGL(k_gather<4>, dim3((1u << 26) / 256), dim3(256), 0, 0, (const uint4*)a, 26, 1u << 26, out);
+        hipLaunchKernelGGL(k_gather_lanes<8>, dim3((1u << 25) * 8 / 256), dim3(256), 0, 0, (const uint4*)a, 25,
+                           1u << 25, out);
+        hipLaunchKernelGGL(k_gather_lanes<4>, dim3((1u << 26) * 4 / 256), dim3(256), 0, 0, (const uint4*)a, 26,
+                           1u << 26, out);
+        // 2^29 slots of 8 B (4 GiB), each written once
+        hipLaunchKernelGGL(k_scatter8, dim3((1u << 29) / 256), dim3(256), 0, 0, (uint64_t*)b, 29, 1u << 29);
+    }
+    CK(hipDeviceSynchronize());
+    printf("\"k_rd<uint4>\": {\"read\": %zu}, \"k_rd<unsigned long>\": {\"read\": %zu}, "
+           "\"k_rd<unsigned int>\": {\"read\": %zu}, \"k_rd12\": {\"read\": %zu}, "
+           "\"k_wr<uint4>\": {\"write\": %zu}, \"k_wr<unsigned long>\": {\"write\": %zu}, "
+           "\"k_gather<8>\": {\"read\": %zu}, \"k_gather<4>\": {\"read\": %zu}, "
+           "\"k_gather_lanes<8>\": {\"read\": %zu}, \"k_gather_lanes<4>\": {\"read\": %zu}, "
+           "\"k_scatter8\": {\"write\": %zu}}}\n",
+           bytes, bytes, bytes, (size_t)12 << 28, bytes, bytes, bytes, bytes, bytes, bytes, bytes);
+    CK(hipFree(a));
+    CK(hipFree(b));
+    CK(hipFree(out));
+    return 0;
+}

@@ -1,17 +1,14 @@
 #!/bin/bash
-# Round-5 iteration: a -k selection of the GPU tests, then bench lines.
-#   tools/r5_iter.sh TAG "pytest -k expr" "configs..."   (configs e.g. "4 2 1"; "-" = none)
+# Full GPU suite (stop at the first failure), then bench lines of the given configs.
+#   tools/r5_full.sh TAG "configs"
 set -o pipefail
-TAG=${1:-iter}
-K=${2:-}
-CFGS=${3:-"4 2 1"}
+TAG=${1:-full}
+CFGS=${2:-"4 2 1"}
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 O=gpurun_out/$TAG
 mkdir -p $O
-if [ -n "$K" ]; then
-  timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -k "$K" > $O/pytest_gpu.log 2>&1
-  rc=$?; echo "PYTEST rc=$rc"; tail -3 $O/pytest_gpu.log; grep -E "FAILED|Error" $O/pytest_gpu.log | head -20; [ $rc -eq 0 ] || exit 1
-fi
+timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1
+rc=$?; echo "PYTEST rc=$rc"; tail -3 $O/pytest_gpu.log; grep -E "FAILED|Error" $O/pytest_gpu.log | head -20; [ $rc -eq 0 ] || exit 1
 [ "$CFGS" = "-" ] && exit 0
 for c in $CFGS; do
   timeout -k 10 300 python bench.py --config $c --steps 10 --warmup 2 --no-cpu-baseline > $O/bench_c$c.json 2> $O/bench_c$c.err || { echo "CONFIG $c FAILED"; tail -5 $O/bench_c$c.err; exit 1; }
