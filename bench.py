@@ -90,7 +90,8 @@ def pmc_traffic_per_launch(config='1'):
     """HBM bytes per face-scan launch of BASELINE config ``config`` at its
     default size, from the newest committed rocprofv3 PMC summary
     (profiles/*/pmc_summary.json for config 1, pmc_summary_c<config>.json for
-    the others; written by tools/pmc_summary.py), or None."""
+    the others; written by tools/pmc_summary.py), the summary's path, and the
+    scan's average duration in that summary's kernel trace (ns) -- or Nones."""
     import glob
     name = 'pmc_summary.json' if config == '1' else 'pmc_summary_c%s.json' % config
     files = sorted(glob.glob(os.path.join(ROOT, 'profiles', '*', name)))
@@ -100,10 +101,10 @@ def pmc_traffic_per_launch(config='1'):
                 d = json.load(fh)
             v = d.get('scan_hbm_bytes_per_launch')
             if v:
-                return float(v), os.path.relpath(f, ROOT)
+                return float(v), os.path.relpath(f, ROOT), d.get('scan_avg_ns')
         except Exception:
             continue
-    return None, None
+    return None, None, None
 
 
 def cpu_baseline(labels_t, bnd_t, planes, workers):
@@ -346,7 +347,7 @@ def bench_config0(args):
         shutil.rmtree(d, ignore_errors=True)
     scan_avg = float(np.mean(scan_ms))
     alg = lo * 12                                   # the feature scan reads every block array (+ halo) once
-    traffic, traffic_src = pmc_traffic_per_launch('0') if not args.cell else (None, None)
+    traffic, traffic_src, _ = pmc_traffic_per_launch('0') if not args.cell else (None, None, None)
     line = {
         'metric': 'Gvoxels/s RAG+edge features (per-block drop-in path, gzip N5 in -> N5 out, uint64 labels, '
                   'float32 boundary map)',
@@ -506,9 +507,9 @@ def main():
     vox_bytes = 8 + 4 * n_ch
     scan_bytes = V * vox_bytes
     achieved = scan_bytes / (scan_avg_ms * 1e-3) / 1e9
-    traffic, traffic_src = (pmc_traffic_per_launch(args.config)
-                            if not args.size and not args.cell and (scaling == 'weak' or world == 1)
-                            else (None, None))
+    traffic, traffic_src, trace_ns = (pmc_traffic_per_launch(args.config)
+                                      if not args.size and not args.cell and (scaling == 'weak' or world == 1)
+                                      else (None, None, None))
     step_bytes = total_vox * vox_bytes + n_edges * EDGE_BYTES
 
     line = None
@@ -544,7 +545,14 @@ def main():
                          'traffic': traffic,
                          'kernel': 'k_narrow_labels + k_face_scan' if narrow_ms > 0 else 'k_face_scan',
                          'kernel_ms': round(scan_avg_ms, 4), 'algorithmic_bytes': scan_bytes,
-                         'traffic_source': traffic_src},
+                         'traffic_source': traffic_src,
+                         # headline 'frac' = this run's HIP events on the scan's stream;
+                         # the committed trace (traffic_source's kernel trace) beside it
+                         'kernel_ms_trace': round(trace_ns / 1e6, 4) if trace_ns else None,
+                         'frac_trace': (round(scan_bytes / (trace_ns * 1e-9) / 1e9 / HBM_PEAK_GBS, 4)
+                                        if trace_ns else None),
+                         'timing': 'frac: HIP events of this run (scan stream); frac_trace: rocprofv3 kernel trace '
+                                   'of the same workload in traffic_source'},
             'step_roofline_frac': round(step_bytes / (ms_step * 1e-3) / 1e9 / (HBM_PEAK_GBS * world), 4),
             'phase_ms': {k: round(v, 4) for k, v in timings.items()},
             'records': n_rec, 'direct_faces': n_direct,

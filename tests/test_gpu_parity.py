@@ -564,6 +564,44 @@ def test_group_sort_matches_other_paths(gpu, monkeypatch, shape, cell, seed):
     check_features(out['features'], f_o)
 
 
+@pytest.mark.parametrize('case', ['boundary', 'ignore', 'graph', 'affinity_lr', 'far_labels'])
+def test_group_sort_cases(gpu, monkeypatch, case):
+    """The group sort path (run table and node bitmap from its run pass:
+    ctg_sort.hip k_gs_runs, node window in LDS) against the onesweep path
+    (CTG_GROUP_SORT=0) and the oracle: boundary maps, ignore_label (kept-edge
+    compaction), graph only, long-range affinities (adjacency filter), and
+    labels spread so that a bucket's node window does not fit LDS (global node
+    atomics)."""
+    lab, bnd = S.generate((40, 72, 100), cell=5, seed=41)
+    kw = {}
+    data = bnd
+    if case == 'ignore':
+        lab = lab.copy()
+        lab[::4, ::3] = 0
+        kw['ignore_label'] = True
+    elif case == 'graph':
+        data = None
+    elif case == 'affinity_lr':
+        kw['offsets'] = S.LR_OFFSETS
+        data = S.affinities_from_boundary(bnd, S.LR_OFFSETS)
+    elif case == 'far_labels':
+        lab = lab * np.uint64(40503) % np.uint64(1 << 29)   # ids scattered over 2^29
+    monkeypatch.setenv('CTG_SORT_PACKED', '0')
+    out = rag.rag_features(lab, data, **kw)
+    monkeypatch.setenv('CTG_GROUP_SORT', '0')
+    monkeypatch.setenv('CTG_BUCKET_SORT_PAIRS', '0')
+    ref = rag.rag_features(lab, data, **kw)
+    np.testing.assert_array_equal(out['edges'], ref['edges'])
+    np.testing.assert_array_equal(out['nodes'], ref['nodes'])
+    if data is not None:
+        np.testing.assert_array_equal(out['features'][:, [2, 8, 9]], ref['features'][:, [2, 8, 9]])
+        np.testing.assert_allclose(out['features'], ref['features'], rtol=1e-12, atol=1e-15)
+    if case in ('boundary', 'ignore', 'far_labels'):
+        e_o, f_o = O.boundary_features(lab, bnd, ignore_label=case == 'ignore')
+        np.testing.assert_array_equal(out['edges'], e_o)
+        check_features(out['features'], f_o)
+
+
 def test_group_sort_one_label_group(gpu, monkeypatch):
     """Every record of one bucket in one in-bucket group (label 1 under a
     plane of ~10 K cells: keys (1, v) only differ in v), and labels >= 2^20 so
