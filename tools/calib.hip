@@ -10,6 +10,9 @@
 //   g128 / g64         random whole-record gathers, one lane per record reading
 //                      8 / 4 16-B pieces (the reduce's 128-B bodies / a 64-B body)
 //   gl8 / gl4          the same records, 8 / 4 lanes per record, 16 B each
+//   gw1 .. gw8         128-B records permuted inside 16 MB windows (TLB-friendly),
+//                      1 / 2 / 4 / 8 lanes per record; gw1 also with 128 MB .. 2 GB
+//                      windows (where TLB reach runs out)
 //   s8                 8-B stores to a random permutation of slots (bucket scatter)
 // Run it under rocprofv3 --kernel-trace and under separate --pmc FETCH_SIZE /
 // WRITE_SIZE passes; tools/calib_summary.py divides the algorithmic bytes by the
@@ -98,6 +101,22 @@ __global__ __launch_bounds__(256) void k_gather_lanes(const uint4* __restrict__ 
     if (fold(v) == 0x12345678u) out[0] = 1u;
 }
 
+// LANES lanes per 128-B record (8 / LANES 16-B pieces each), records permuted
+// inside 16 MB windows (2^17 records): TLB-friendly, like the reduction's
+// gathers of records written by neighbouring tiles
+template <int LANES, int WB = 17>
+__global__ __launch_bounds__(256) void k_gather_win(const uint4* __restrict__ rec, uint32_t n, uint32_t* out) {
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n * LANES) return;
+    const uint32_t r = i / LANES, l = i % LANES;
+    const uint32_t rr = (r & ~((1u << WB) - 1u)) | perm_k(r & ((1u << WB) - 1u), WB);
+    const uint4* b = rec + (size_t)rr * 8 + l * (8 / LANES);
+    uint32_t acc = 0;
+#pragma unroll
+    for (int j = 0; j < 8 / LANES; ++j) acc ^= fold(b[j]);
+    if (acc == 0x12345678u) out[0] = 1u;
+}
+
 __global__ __launch_bounds__(256) void k_scatter8(uint64_t* __restrict__ p, int k, uint32_t n) {
     const uint32_t i = blockIdx.x * 256 + threadIdx.x;
     if (i < n) p[perm_k(i, k)] = (uint64_t)i;
@@ -131,6 +150,14 @@ int main(int argc, char** argv) {
                            1u << 25, out);
         hipLaunchKernelGGL(k_gather_lanes<4>, dim3((1u << 26) * 4 / 256), dim3(256), 0, 0, (const uint4*)a, 26,
                            1u << 26, out);
+        hipLaunchKernelGGL(k_gather_win<1>, dim3((1u << 25) / 256), dim3(256), 0, 0, (const uint4*)a, 1u << 25, out);
+        hipLaunchKernelGGL(k_gather_win<2>, dim3((1u << 25) * 2 / 256), dim3(256), 0, 0, (const uint4*)a, 1u << 25, out);
+        hipLaunchKernelGGL(k_gather_win<4>, dim3((1u << 25) * 4 / 256), dim3(256), 0, 0, (const uint4*)a, 1u << 25, out);
+        hipLaunchKernelGGL(k_gather_win<8>, dim3((1u << 25) * 8 / 256), dim3(256), 0, 0, (const uint4*)a, 1u << 25, out);
+        hipLaunchKernelGGL((k_gather_win<1, 20>), dim3((1u << 25) / 256), dim3(256), 0, 0, (const uint4*)a, 1u << 25, out);
+        hipLaunchKernelGGL((k_gather_win<1, 22>), dim3((1u << 25) / 256), dim3(256), 0, 0, (const uint4*)a, 1u << 25, out);
+        hipLaunchKernelGGL((k_gather_win<1, 23>), dim3((1u << 25) / 256), dim3(256), 0, 0, (const uint4*)a, 1u << 25, out);
+        hipLaunchKernelGGL((k_gather_win<1, 24>), dim3((1u << 25) / 256), dim3(256), 0, 0, (const uint4*)a, 1u << 25, out);
         // 2^29 slots of 8 B (4 GiB), each written once
         hipLaunchKernelGGL(k_scatter8, dim3((1u << 29) / 256), dim3(256), 0, 0, (uint64_t*)b, 29, 1u << 29);
     }
@@ -140,8 +167,13 @@ int main(int argc, char** argv) {
            "\"k_wr<uint4>\": {\"write\": %zu}, \"k_wr<unsigned long>\": {\"write\": %zu}, "
            "\"k_gather<8>\": {\"read\": %zu}, \"k_gather<4>\": {\"read\": %zu}, "
            "\"k_gather_lanes<8>\": {\"read\": %zu}, \"k_gather_lanes<4>\": {\"read\": %zu}, "
+           "\"k_gather_win<1, 17>\": {\"read\": %zu}, \"k_gather_win<2, 17>\": {\"read\": %zu}, "
+           "\"k_gather_win<4, 17>\": {\"read\": %zu}, \"k_gather_win<8, 17>\": {\"read\": %zu}, "
+           "\"k_gather_win<1, 20>\": {\"read\": %zu}, \"k_gather_win<1, 22>\": {\"read\": %zu}, "
+           "\"k_gather_win<1, 23>\": {\"read\": %zu}, \"k_gather_win<1, 24>\": {\"read\": %zu}, "
            "\"k_scatter8\": {\"write\": %zu}}}\n",
-           bytes, bytes, bytes, (size_t)12 << 28, bytes, bytes, bytes, bytes, bytes, bytes, bytes);
+           bytes, bytes, bytes, (size_t)12 << 28, bytes, bytes, bytes, bytes, bytes, bytes, bytes, bytes, bytes, bytes,
+           bytes, bytes, bytes, bytes, bytes);
     CK(hipFree(a));
     CK(hipFree(b));
     CK(hipFree(out));
