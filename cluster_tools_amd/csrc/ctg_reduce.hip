@@ -207,7 +207,14 @@ __global__ __launch_bounds__(256) void k_reduce_edges(int64_t E, const uint32_t*
         } else
 #endif
         {
-            for (uint32_t r = b; r < b + n; ++r) load_record<WIDE>(R, perm(r), h, cnt, flags, mn, mx, mo);
+            // the next slot index is loaded while this record's body is in
+            // flight: one global latency per record instead of two
+            uint32_t i = n ? perm(b) : 0u;
+            for (uint32_t r = b; r < b + n; ++r) {
+                const uint32_t nxt = r + 1 < b + n ? perm(r + 1) : 0u;
+                load_record<WIDE>(R, i, h, cnt, flags, mn, mx, mo);
+                i = nxt;
+            }
         }
         reduce_epilogue(e, u, h, cnt, flags, mn, mx, mo, umask, need_adj, ignore_label, scale, offset, O);
     }
@@ -244,18 +251,17 @@ __global__ void k_endpoints(int64_t E, const uint64_t* __restrict__ uniq, int nb
     out[2 * e + 1] = (uint32_t)(sk & ((1ull << nb) - 1ull));
 }
 
+// one thread per label of the bitmap: a set bit's rank among the set bits
+// before it is its node position, so consecutive nodes are stored by
+// consecutive lanes (a per-word expansion loop stores 32 scattered u64 per lane)
 __global__ void k_bits_to_nodes(int64_t W, const uint32_t* __restrict__ bits, const uint32_t* __restrict__ off,
                                 uint64_t* __restrict__ nodes, uint32_t* __restrict__ dN) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= W) return;
-    uint32_t b = bits[i];
-    uint32_t o = off[i];
-    if (i == W - 1) *dN = o + __popc(b);   // node count
-    while (b) {
-        const int k = __ffs(b) - 1;
-        nodes[o++] = (uint64_t)(i * 32 + k);
-        b &= b - 1;
-    }
+    if (i >= W * 32) return;
+    const int64_t w = i >> 5;
+    const uint32_t b = bits[w], k = (uint32_t)(i & 31);
+    if (i == W * 32 - 1) *dN = off[w] + __popc(b);   // node count
+    if ((b >> k) & 1u) nodes[off[w] + __popc(b & ((1u << k) - 1u))] = (uint64_t)i;
 }
 
 // Nodes as a bitmap over [0, max label], built per chunk of the sorted key
@@ -273,38 +279,54 @@ constexpr int NODE_WORDS = 8192;   // 32 KB LDS window = 262144 labels
 __global__ __launch_bounds__(256) void k_mark_nodes_win(int64_t E, const uint32_t* __restrict__ dE,
                                                         const uint64_t* __restrict__ uniq, int nb,
                                                         uint32_t* __restrict__ bits) {
+    constexpr int PER = NODE_CHUNK / 256;
     __shared__ uint32_t bm[NODE_WORDS];
     __shared__ uint32_t red[4];
-    const int tid = threadIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63;
     E = min(E, (int64_t)*dE);
     const int64_t e0 = (int64_t)blockIdx.x * NODE_CHUNK;
     if (e0 >= E) return;
     const int64_t e1 = min(E, e0 + NODE_CHUNK);
     const uint64_t vmask = (1ull << nb) - 1ull;
-    const uint32_t base = (uint32_t)(uniq[e0] >> nb) & ~31u;   // v > u >= u(e0)
+    // each key is read once: kept in registers for the window bound and the marks
+    uint64_t sk[PER];
     uint32_t vmax = 0;
-    for (int64_t e = e0 + tid; e < e1; e += 256) vmax = max(vmax, (uint32_t)(uniq[e] & vmask));
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+        const int64_t e = e0 + tid + 256 * k;
+        sk[k] = e < e1 ? uniq[e] : 0ull;
+        vmax = max(vmax, (uint32_t)(sk[k] & vmask));
+    }
+    const uint32_t base = (uint32_t)(uniq[e0] >> nb) & ~31u;   // v > u >= u(e0)
     for (int o = 32; o > 0; o >>= 1) vmax = max(vmax, (uint32_t)__shfl_xor((int)vmax, o, 64));
-    if ((tid & 63) == 0) red[tid >> 6] = vmax;
-    for (int w = tid; w < NODE_WORDS; w += 256) bm[w] = 0u;
+    if (lane == 0) red[tid >> 6] = vmax;
     __syncthreads();
     vmax = max(max(red[0], red[1]), max(red[2], red[3]));
     const uint32_t nw = ((vmax - base) >> 5) + 1;
-    if (nw > (uint32_t)NODE_WORDS) {
-        for (int64_t e = e0 + tid; e < e1; e += 256) {
-            const uint64_t sk = uniq[e];
-            const uint32_t u = (uint32_t)(sk >> nb), v = (uint32_t)(sk & vmask);
-            if (e == 0 || (uint32_t)(uniq[e - 1] >> nb) != u) atomicOr(&bits[u >> 5], 1u << (u & 31));
-            atomicOr(&bits[v >> 5], 1u << (v & 31));
+    const bool win = nw <= (uint32_t)NODE_WORDS;
+    if (win) {   // clear only the window this chunk uses
+        for (uint32_t w = tid; w < nw; w += 256) bm[w] = 0u;
+        __syncthreads();
+    }
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+        const int64_t e = e0 + tid + 256 * k;
+        const uint32_t u = (uint32_t)(sk[k] >> nb), v = (uint32_t)(sk[k] & vmask);
+        // u is sorted: only a run head marks it (the previous key is the
+        // previous lane's, or a reload for the wave's first lane)
+        uint32_t up = (uint32_t)__shfl_up((int)u, 1, 64);
+        if (lane == 0) up = e > 0 ? (uint32_t)(uniq[e - 1] >> nb) : ~u;
+        if (e < e1) {
+            if (win) {
+                if (up != u) atomicOr(&bm[(u - base) >> 5], 1u << ((u - base) & 31));
+                atomicOr(&bm[(v - base) >> 5], 1u << ((v - base) & 31));
+            } else {
+                if (up != u) atomicOr(&bits[u >> 5], 1u << (u & 31));
+                atomicOr(&bits[v >> 5], 1u << (v & 31));
+            }
         }
-        return;
     }
-    for (int64_t e = e0 + tid; e < e1; e += 256) {
-        const uint64_t sk = uniq[e];
-        const uint32_t u = (uint32_t)(sk >> nb) - base, v = (uint32_t)(sk & vmask) - base;
-        if (e == 0 || (uint32_t)(uniq[e - 1] >> nb) != u + base) atomicOr(&bm[u >> 5], 1u << (u & 31));
-        atomicOr(&bm[v >> 5], 1u << (v & 31));
-    }
+    if (!win) return;
     __syncthreads();
     for (uint32_t w = tid; w < nw; w += 256) {
         const uint32_t b = bm[w];
@@ -321,7 +343,7 @@ hipError_t launch_mark_nodes(int64_t E, const uint32_t* dE, const uint64_t* uniq
 }
 hipError_t launch_bits_to_nodes(int64_t W, const uint32_t* bits, const uint32_t* off, uint64_t* nodes, uint32_t* dN,
                                 hipStream_t s) {
-    hipLaunchKernelGGL(k_bits_to_nodes, dim3((unsigned)((W + 255) / 256)), dim3(256), 0, s, W, bits, off, nodes, dN);
+    hipLaunchKernelGGL(k_bits_to_nodes, dim3((unsigned)((W * 32 + 255) / 256)), dim3(256), 0, s, W, bits, off, nodes, dN);
     return hipGetLastError();
 }
 
