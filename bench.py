@@ -79,6 +79,10 @@ def parse():
     # exchange over gloo (the driver's multi-GPU runs use the defaults: RCCL,
     # device = LOCAL_RANK)
     p.add_argument('--backend', default='nccl', choices=['nccl', 'gloo'])
+    p.add_argument('--write-output', default=None, metavar='DIR',
+                   help='multi-GPU path: after the timed steps, gather the last step\'s shards on rank 0 and write '
+                        'graph / features N5 under DIR (dist.write_global, SURVEY 8(e) Output); reported as '
+                        '"output" beside the line, outside the timed region')
     p.add_argument('--dist-path', action='store_true',
                    help='run the multi-GPU step (cluster_tools_amd/dist.py: splitters, all_to_all exchange, merge) '
                         'even at WORLD_SIZE 1 -- an RCCL rehearsal on a one-GPU box (launch under torch.distributed.run)')
@@ -512,6 +516,19 @@ def main():
                                       else (None, None, None))
     step_bytes = total_vox * vox_bytes + n_edges * EDGE_BYTES
 
+    output = None
+    if use_dist and args.write_output:   # SURVEY 8(e) Output, outside the timed region
+        ot = {}
+        dist.barrier()
+        w = cdist.write_global(res, os.path.join(args.write_output, 'graph.n5'), 'graph',
+                               os.path.join(args.write_output, 'features.n5'), 'features', shape=list(gshape),
+                               root=0, timings=ot)
+        if rank == 0:
+            output = {'gather_s': round(ot.get('gather_s', 0.0), 4), 'n5_write_s': round(ot.get('write_s', 0.0), 4),
+                      'edges': w[0], 'nodes': w[1], 'path': args.write_output,
+                      'what': 'dist.gather_to_host of the last step\'s shards on rank 0, then graph/{nodes,edges} '
+                              '+ features N5 datasets as MergeSubGraphs / MergeEdgeFeatures write them'}
+
     line = None
     if rank == 0:
         cpu = None
@@ -560,6 +577,8 @@ def main():
                 cdist.host_reads))} if use_dist else None),
             'cpu_baseline': cpu,
         }
+        if output is not None:
+            line['output'] = output
         print(json.dumps(line), flush=True)
     res.free()
     if use_dist:

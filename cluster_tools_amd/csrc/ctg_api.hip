@@ -269,7 +269,7 @@ using RecordSortConfig = rocprim::default_config;
 // records at 512^3: 0.185 -> 0.151 ms; 27.8 M at 2048^3: 1.88 -> 1.49 ms) and
 // lose for very large ones (298 M records of configs[4]:
 // 14.1 -> 18.7 ms, the 1024-way scatter coalesces worse), so they are used up
-// to this many records (CTG_SORT_WIDE_MAX overrides).
+// to this many records.
 static bool sort_packed() {
     const char* e = getenv("CTG_SORT_PACKED");   // read per call: tests switch it
     return !(e && e[0] == '0');

@@ -87,7 +87,7 @@ bool read_file(const std::string& path, std::vector<unsigned char>& buf, bool& m
 // level, producing ordinary gzip / zlib streams.  Chunks are whole buffers of
 // known decoded size, which is exactly libdeflate's interface.  Absent library
 // or a stream it refuses (e.g. multi-member gzip): zlib below.
-// CTG_IO_ZLIB_ONLY=1 forces zlib (A/B).
+
 struct Deflate {
     void* (*alloc_c)(int) = nullptr;
     void (*free_c)(void*) = nullptr;
@@ -100,8 +100,6 @@ struct Deflate {
     int (*zlib_d)(void*, const void*, size_t, void*, size_t, size_t*) = nullptr;
     bool ok = false;
     Deflate() {
-        const char* env = std::getenv("CTG_IO_ZLIB_ONLY");
-        if (env && env[0] == '1') return;
         void* h = dlopen("libdeflate.so.0", RTLD_NOW | RTLD_LOCAL);
         if (!h) return;
         alloc_c = (void* (*)(int))dlsym(h, "libdeflate_alloc_compressor");
@@ -503,7 +501,7 @@ ChunkPtr get_chunk(const std::string& path, int format, int ndim, const int64_t*
 // one stride past this one -- the stride being the step between this thread's
 // last two reads of the dataset -- and the next box in C order before a
 // stride is known.  A guess outside the chunk grid (the stride wrapping to the
-// next row) queues nothing.  CTG_IO_READAHEAD=0 disables it.
+// next row) queues nothing.  CTG_IO_CACHE_MB=0 disables it.
 // ---------------------------------------------------------------------------
 class Prefetcher {
 public:
@@ -555,13 +553,7 @@ private:
     bool stop_ = false;
 };
 
-bool readahead_on() {
-    static const bool on = [] {
-        const char* e = getenv("CTG_IO_READAHEAD");
-        return !(e && e[0] == '0');
-    }();
-    return on && cache_budget() > 0;
-}
+bool readahead_on() { return cache_budget() > 0; }   // (CTG_IO_CACHE_MB=0 turns both off)
 
 // (dataset, thread) -> the chunk origin of that thread's previous box read
 struct LastBox {

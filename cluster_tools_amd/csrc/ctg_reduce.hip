@@ -122,11 +122,12 @@ struct Perm {
     }
 };
 
-// per-edge epilogue of the reduce: keep flag, mergeable stats row, features
+// per-edge epilogue of the reduce: keep flag, mergeable stats row; the feature
+// row is returned in registers (k_reduce_edges stages it for coalesced stores)
 __device__ __forceinline__ void reduce_epilogue(int64_t e, uint64_t u, uint32_t (&h)[NSLOTS], uint32_t cnt,
                                                 uint32_t flags, uint32_t mn, uint32_t mx, const Moments& mo,
                                                 uint64_t umask, int need_adj, int ignore_label, double scale,
-                                                double offset, const ReduceOut& O) {
+                                                double offset, const ReduceOut& O, double2 (&row)[5]) {
     const double sum = mo.S1, sq = mo.S2;   // about the pivot mo.p0
     // need_adj: 0 every record is an edge (boundary maps), 1 keep edges seen
     // on a nearest-neighbour face, 2 keep all and carry the flag (partials)
@@ -148,19 +149,33 @@ __device__ __forceinline__ void reduce_epilogue(int64_t e, uint64_t u, uint32_t 
         O.wsums[e] = make_double2(sum, sq);
     }
     if (!O.feats) return;
-    double* o = O.feats + (size_t)e * N_FEATURES;
 #ifdef CTG_DIAG
-    if (O.ablate & 4) {   // keep the values live without the 80-B row stores
-        double t = sum + sq + (double)cnt + (double)mn + (double)mx;
-#pragma unroll
-        for (int j = 0; j < NSLOTS; ++j) t += (double)h[j];
-        if (t == -1.0) o[0] = t;
-        return;
-    }
-    finalize_row(h, cnt, mn, mx, mo, scale, offset, o, !(O.ablate & 1));
+    finalize_vals(h, cnt, mn, mx, mo, scale, offset, row, !(O.ablate & 1));
 #else
-    finalize_row(h, cnt, mn, mx, mo, scale, offset, o);
+    finalize_vals(h, cnt, mn, mx, mo, scale, offset, row);
 #endif
+}
+
+// A wave's 64 feature rows (80 B each, lane = edge) go out through LDS: lane l
+// writes its five 16-B column pairs to stage[5 l + j], then store k of the
+// wave writes pairs [64 k, 64 k + 64) of the wave's contiguous 5120-B block --
+// five fully coalesced stores instead of five 64-lane scatters at an 80-B
+// stride.  Rows at or past `n` (the tail wave) are not stored.
+__device__ __forceinline__ void store_rows_staged(double2* __restrict__ stage, const double2 (&row)[5],
+                                                  double2* __restrict__ out, int64_t e0, int64_t n) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int j = 0; j < N_FEATURES / 2; ++j) stage[5 * lane + j] = row[j];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+    const int64_t lim = (min(n - e0, (int64_t)64)) * (N_FEATURES / 2);
+    double2* o = out + e0 * (N_FEATURES / 2);
+#pragma unroll
+    for (int k = 0; k < N_FEATURES / 2; ++k) {
+        const int q = 64 * k + lane;
+        if (q < lim) o[q] = stage[q];
+    }
 }
 
 template <bool WIDE, bool STATS>
@@ -173,13 +188,14 @@ __global__ __launch_bounds__(256) void k_reduce_edges(int64_t E, const uint32_t*
                                                       ReduceOut O) {
     const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (e == 0 && O.count_out) *O.count_out = *dE;
-    if (e >= E || e >= (int64_t)*dE) return;
-    const uint64_t sk = uniq[e];
-    const uint64_t u = sk >> nb, v = sk & ((1ull << nb) - 1ull);
-    O.edges[2 * e] = u;
-    O.edges[2 * e + 1] = v;
-    uint32_t flags = 0;
+    const int64_t En = min(E, (int64_t)*dE);
     if constexpr (!STATS) {
+        if (e >= En) return;
+        const uint64_t sk = uniq[e];
+        const uint64_t u = sk >> nb, v = sk & ((1ull << nb) - 1ull);
+        O.edges[2 * e] = u;
+        O.edges[2 * e + 1] = v;
+        uint32_t flags = 0;
         if (need_adj) {
             const uint32_t b = offs[e], n = runs[e];
             for (uint32_t r = b; r < b + n; ++r) {
@@ -192,31 +208,53 @@ __global__ __launch_bounds__(256) void k_reduce_edges(int64_t E, const uint32_t*
         if (O.keep) O.keep[e] = ((flags & ADJ_FLAG) || need_adj != 1) && !(ignore_label && (u & umask) == 0) ? 1u : 0u;
         return;
     } else {
-        uint32_t h[NSLOTS];
+        __shared__ double2 stage[256 / 64][64 * (N_FEATURES / 2)];
+        const int64_t e0 = e - (threadIdx.x & 63);   // the wave's first edge
+        if (e0 >= En) return;                       // (uniform per wave)
+        double2 row[5];
+        if (e < En) {
+            const uint64_t sk = uniq[e];
+            const uint64_t u = sk >> nb, v = sk & ((1ull << nb) - 1ull);
+            O.edges[2 * e] = u;
+            O.edges[2 * e + 1] = v;
+            uint32_t flags = 0;
+            uint32_t h[NSLOTS];
 #pragma unroll
-        for (int j = 0; j < NSLOTS; ++j) h[j] = 0;
-        uint32_t cnt = 0, mn = ORD_POS_INF, mx = ORD_NEG_INF;
-        Moments mo;
-        const uint32_t b = offs[e], n = runs[e];
+            for (int j = 0; j < NSLOTS; ++j) h[j] = 0;
+            uint32_t cnt = 0, mn = ORD_POS_INF, mx = ORD_NEG_INF;
+            Moments mo;
+            const uint32_t b = offs[e], n = runs[e];
 #ifdef CTG_DIAG   // diagnostic ablation (CTG_REDUCE_ABLATE, variant builds only)
-        if (O.ablate & 2) {
-            cnt = n;
-            h[1] = n;
-            mn = mx = 0x3F800000u ^ 0x80000000u;
-            mo.add(n, 0.0, 0.0, 0u);
-        } else
+            if (O.ablate & 2) {
+                cnt = n;
+                h[1] = n;
+                mn = mx = 0x3F800000u ^ 0x80000000u;
+                mo.add(n, 0.0, 0.0, 0u);
+            } else
 #endif
-        {
-            // the next slot index is loaded while this record's body is in
-            // flight: one global latency per record instead of two
-            uint32_t i = n ? perm(b) : 0u;
-            for (uint32_t r = b; r < b + n; ++r) {
-                const uint32_t nxt = r + 1 < b + n ? perm(r + 1) : 0u;
-                load_record<WIDE>(R, i, h, cnt, flags, mn, mx, mo);
-                i = nxt;
+            {
+                // the next slot index is loaded while this record's body is in
+                // flight: one global latency per record instead of two
+                uint32_t i = n ? perm(b) : 0u;
+                for (uint32_t r = b; r < b + n; ++r) {
+                    const uint32_t nxt = r + 1 < b + n ? perm(r + 1) : 0u;
+                    load_record<WIDE>(R, i, h, cnt, flags, mn, mx, mo);
+                    i = nxt;
+                }
             }
+            reduce_epilogue(e, u, h, cnt, flags, mn, mx, mo, umask, need_adj, ignore_label, scale, offset, O, row);
         }
-        reduce_epilogue(e, u, h, cnt, flags, mn, mx, mo, umask, need_adj, ignore_label, scale, offset, O);
+        if (!O.feats) return;
+#ifdef CTG_DIAG
+        if (O.ablate & 4) {   // keep the values live without the row stores
+            double t = 0.0;
+#pragma unroll
+            for (int j = 0; j < 5; ++j) t += row[j].x + row[j].y;
+            if (t == -1.0) O.feats[0] = t;
+            return;
+        }
+#endif
+        store_rows_staged(stage[threadIdx.x >> 6], row, reinterpret_cast<double2*>(O.feats), e0, En);
     }
 }
 

@@ -167,15 +167,14 @@ struct Moments {
 };
 
 // The 10 feature columns of one edge from its combined statistics (count, the
-// 42-slot histogram, ordered min / max, shifted sums about mo.p0); an edge
-// without samples gets a zero row.  `o` is 16-B aligned (five 16-B stores).
-__device__ __forceinline__ void finalize_row(const uint32_t (&h)[NSLOTS], uint32_t cnt, uint32_t mn, uint32_t mx,
-                                             const Moments& mo, double scale, double offset, double* __restrict__ o,
-                                             bool quantiles = true) {
-    double2* o2 = reinterpret_cast<double2*>(o);
+// 42-slot histogram, ordered min / max, shifted sums about mo.p0) as five
+// column pairs in registers; an edge without samples gets a zero row.
+__device__ __forceinline__ void finalize_vals(const uint32_t (&h)[NSLOTS], uint32_t cnt, uint32_t mn, uint32_t mx,
+                                              const Moments& mo, double scale, double offset, double2 (&r)[5],
+                                              bool quantiles = true) {
     if (cnt == 0) {
 #pragma unroll
-        for (int j = 0; j < N_FEATURES / 2; ++j) o2[j] = make_double2(0.0, 0.0);
+        for (int j = 0; j < N_FEATURES / 2; ++j) r[j] = make_double2(0.0, 0.0);
         return;
     }
     const double sum = mo.S1, sq = mo.S2;   // about the pivot mo.p0
@@ -191,11 +190,22 @@ __device__ __forceinline__ void finalize_row(const uint32_t (&h)[NSLOTS], uint32
     const double vmin = (double)ord2f(mn), vmax = (double)ord2f(mx);
     double qv[5] = {0.0, 0.0, 0.0, 0.0, 0.0};   // registers (constant indices after unrolling)
     if (quantiles) vigra_quantiles_cross(h, c, vmin, vmax, scale, offset, qv);
-    o2[0] = make_double2(mean, var);
-    o2[1] = make_double2(vmin, qv[0]);
-    o2[2] = make_double2(qv[1], qv[2]);
-    o2[3] = make_double2(qv[3], qv[4]);
-    o2[4] = make_double2(vmax, c);
+    r[0] = make_double2(mean, var);
+    r[1] = make_double2(vmin, qv[0]);
+    r[2] = make_double2(qv[1], qv[2]);
+    r[3] = make_double2(qv[3], qv[4]);
+    r[4] = make_double2(vmax, c);
+}
+
+// the same row stored at o (16-B aligned: five 16-B stores)
+__device__ __forceinline__ void finalize_row(const uint32_t (&h)[NSLOTS], uint32_t cnt, uint32_t mn, uint32_t mx,
+                                             const Moments& mo, double scale, double offset, double* __restrict__ o,
+                                             bool quantiles = true) {
+    double2 r[5];
+    finalize_vals(h, cnt, mn, mx, mo, scale, offset, r, quantiles);
+    double2* o2 = reinterpret_cast<double2*>(o);
+#pragma unroll
+    for (int j = 0; j < N_FEATURES / 2; ++j) o2[j] = r[j];
 }
 
 // one wide statistics record (48 words: 42 slots, count|ADJ, ordered min,

@@ -4,10 +4,12 @@ usage: python tools/pmc_summary.py <trace_dir> <pmc_dir_fetch> <pmc_dir_write> <
 
 * kernel stats: <trace_dir>/**/*kernel_stats.csv (Name, Calls, AverageNs ...)
 * PMC: <pmc_dir>/**/*counter_collection.csv, one row per (dispatch, counter)
-FETCH_SIZE / WRITE_SIZE are in KiB per dispatch.  gfx950 tallies 128-B read
-requests at 64 B (MI355X_MICROARCH.md, HBM section), so the HBM read bytes of
-a coalesced stream are 2 x FETCH_SIZE x 1024; the factor is re-derived from
-the loads-only ablation of the face scan when that pass is present.
+FETCH_SIZE / WRITE_SIZE are in KiB per dispatch.  The factors that turn them
+into HBM bytes come from the counter calibration (tools/calib.hip ->
+profiles/r5/calib.json): every read shape the face scan uses
+(8-B label and 4-B sample loads per lane, the 8 + 4 B pair, 16-B pieces) and
+the 128-B record gathers measure FETCH factor 2.000; the 16-B and 8-B stores
+WRITE factor 1.000.  The scan's factors are taken from that file when present.
 """
 import csv
 import glob
@@ -51,8 +53,28 @@ def pick(d, sub):
     return max(vals) if vals else None
 
 
+CALIB = os.path.join(os.path.dirname(os.path.abspath(__file__)), '..', 'profiles', 'r5', 'calib.json')
+# the calibration kernels standing for the face scan's access shapes
+SCAN_READS = ('k_rd<unsigned long>', 'k_rd<unsigned int>', 'k_rd12', 'k_rd<uint4>')
+SCAN_WRITES = ('k_wr<uint4>', 'k_wr<unsigned long>')
+
+
+def factors():
+    """(read factor, write factor, provenance) for the scan's access shapes."""
+    try:
+        k = json.load(open(CALIB))['kernels']
+        rf = [k[n]['factor'] for n in SCAN_READS if 'factor' in k.get(n, {})]
+        wf = [k[n]['factor'] for n in SCAN_WRITES if 'factor' in k.get(n, {})]
+    except (OSError, ValueError, KeyError):
+        rf = wf = []
+    if rf and wf and max(rf) - min(rf) < 0.02 and max(wf) - min(wf) < 0.02:
+        return sum(rf) / len(rf), sum(wf) / len(wf), 'profiles/r5/calib.json ' + ', '.join(SCAN_READS + SCAN_WRITES)
+    return 2.0, 1.0, 'uncalibrated default (MI355X_MICROARCH.md HBM section)'
+
+
 def main():
     trace, pf, pw, out = sys.argv[1:5]
+    rfac, wfac, fsrc = factors()
     alg = float(sys.argv[5]) if len(sys.argv) > 5 else None
     sha = sys.argv[6] if len(sys.argv) > 6 else None
     stats = kernel_stats(trace)
@@ -64,8 +86,10 @@ def main():
         'kernel_stats': stats,
         'fetch_size_kib_per_dispatch': fetch,
         'write_size_kib_per_dispatch': write,
-        'read_factor': 2.0,
-        'note': 'HBM bytes = 2 x FETCH_SIZE x 1024 + WRITE_SIZE x 1024 (gfx950 FETCH_SIZE halving)',
+        'read_factor': rfac,
+        'write_factor': wfac,
+        'factor_source': fsrc,
+        'note': 'HBM bytes = read_factor x FETCH_SIZE x 1024 + write_factor x WRITE_SIZE x 1024',
         'git_sha': sha,
     }
     # the face scan's average duration from the kernel trace (the launched
@@ -89,9 +113,9 @@ def main():
         scan_w = (scan_w or 0.0) + (nar_w or 0.0)
         summary['includes_k_narrow_labels'] = True
     if scan_f is not None and scan_w is not None:
-        summary['scan_hbm_bytes_per_launch'] = 2.0 * scan_f * 1024 + scan_w * 1024
-        summary['scan_read_bytes_per_launch'] = 2.0 * scan_f * 1024
-        summary['scan_write_bytes_per_launch'] = scan_w * 1024
+        summary['scan_hbm_bytes_per_launch'] = rfac * scan_f * 1024 + wfac * scan_w * 1024
+        summary['scan_read_bytes_per_launch'] = rfac * scan_f * 1024
+        summary['scan_write_bytes_per_launch'] = wfac * scan_w * 1024
         if alg:
             summary['scan_algorithmic_bytes'] = alg
             summary['scan_traffic_over_algorithmic'] = summary['scan_hbm_bytes_per_launch'] / alg

@@ -28,6 +28,9 @@ elif mode == 'graph':
 torch.cuda.synchronize()
 for _ in range(int(os.environ.get('CTG_PROF_ITERS', '3'))):
     r = rag.rag_features_handle(lab, data, offsets=offsets)
+    n_rec, n_direct = r.info()
     r.free()
 torch.cuda.synchronize()
-print('done', mode)
+# records x (8-B key + 128-B body): the scan's nominal record writes, to set
+# beside its WRITE_SIZE
+print('done', mode, 'records=%d direct_faces=%d record_bytes=%d' % (n_rec, n_direct, n_rec * 136))

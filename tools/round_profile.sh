@@ -49,6 +49,7 @@ for c in $CONFIGS; do
     fi || { echo "TRACE_c${c} FAILED"; exit 1; }
     echo "TRACE_c${c}_OK $(cat $O/bench_traced_c$c.json)"
     CTG_PROF_SIZE=$S CTG_PROF_CELL=$CELL CTG_PROF_ITERS=2 pmc c$c python tools/prof_scan.py $MODE || exit 1
+    grep -h "^done" $O/pmc_write_c$c.log > $O/records_c$c.txt || true
   fi
   python tools/pmc_summary.py $O/trace_c$c $O/pmc_fetch_c$c $O/pmc_write_c$c $O/pmc_summary$SUF.json $ALG "$SHA" ||
       exit 1
