@@ -384,10 +384,11 @@ __device__ __forceinline__ int bucket_match(const uint4& b01, const uint4& b23, 
 }
 
 // statistics of one staged entry into table slot s (s < 0: direct record);
-// pv: the slot's pivot word as read by the batch (PIV_EMPTY: none yet)
+// pv: the slot's pivot word as read by the batch (PIV_EMPTY: none yet); cur:
+// its ordered (min, max) as read by the batch
 template <int MODE, bool FAST40, bool BATCH, typename StageT>
-__device__ __forceinline__ void fold_stats(Table& T, const StageT& e, int s, uint32_t pv, RecordBuf R, Counters* C,
-                                           double scale, double offset, bool& need, int ablate) {
+__device__ __forceinline__ void fold_stats(Table& T, const StageT& e, int s, uint32_t pv, uint2 cur, RecordBuf R,
+                                           Counters* C, double scale, double offset, bool& need, int ablate) {
     constexpr bool BND = MODE == MODE_BOUNDARY;
     constexpr bool AFF = MODE == MODE_AFFINITY || MODE == MODE_AFF_MIX;
     const uint64_t key = ((uint64_t)e.x << 32) | e.y;
@@ -431,8 +432,8 @@ __device__ __forceinline__ void fold_stats(Table& T, const StageT& e, int s, uin
         // keeps every count, hence every u16 histogram slot, below 2^16.  The
         // ones that do not need the pivot go first, so the batch's pivot reads
         // land behind them.
-        atomicMin(&T.w[s][22], mn);
-        atomicMax(&T.w[s][23], mx);
+        if (mn < cur.x) atomicMin(&T.w[s][22], mn);
+        if (mx > cur.y) atomicMax(&T.w[s][23], mx);
         // word 21 carries only the ADJ flag in the table; the count is the
         // histogram's sum, filled in by the flush
         if (nnf) atomicOr(&T.w[s][21], ADJ_FLAG);
@@ -490,8 +491,8 @@ __device__ __forceinline__ double dpp_f64(double v) {
 // rarely share a slot within a quad, and the exchanges lengthen every fold)
 template <int MODE, bool FAST40, bool BATCH, typename StageT, int NPER>
 __device__ __forceinline__ void fold_grouped(Table& T, const StageT (&e)[NPER], const int (&slot)[NPER],
-                                             const uint32_t (&pv)[NPER], int lane, RecordBuf R, Counters* C,
-                                             double scale, double offset, int ablate) {
+                                             const uint32_t (&pv)[NPER], const uint2 (&mm)[NPER], int lane,
+                                             RecordBuf R, Counters* C, double scale, double offset, int ablate) {
     constexpr bool BND = MODE == MODE_BOUNDARY;
     constexpr bool AFF = MODE == MODE_AFFINITY || MODE == MODE_AFF_MIX;
 #pragma unroll
@@ -499,7 +500,8 @@ __device__ __forceinline__ void fold_grouped(Table& T, const StageT (&e)[NPER], 
         const int sl = slot[i];
         if (sl == -1) {   // table full: a direct record, no grouping (rare)
             bool dummy = false;
-            fold_stats<MODE, FAST40, BATCH, StageT>(T, e[i], -1, PIV_EMPTY, R, C, scale, offset, dummy, 0);
+            fold_stats<MODE, FAST40, BATCH, StageT>(T, e[i], -1, PIV_EMPTY, make_uint2(ORD_POS_INF, ORD_NEG_INF), R, C,
+                                                    scale, offset, dummy, 0);
         }
         // adjacency-only entries (fold_stats' rule): the flag, no samples, no group
         const bool adj = (AFF || BATCH) && e[i].w == MARK_ADJ && (AFF || e[i].z == MARK_ADJ);
@@ -548,11 +550,15 @@ __device__ __forceinline__ void fold_grouped(Table& T, const StageT (&e)[NPER], 
         }
         const bool lead = !(g1 && (lane & 1));
         if (v && lead && !(ablate & 2048)) {   // (diagnostic 2048: no moment / min / max atomics)
-            atomicMin(&T.w[sl][22], mn);
-            atomicMax(&T.w[sl][23], mx);
+            if (!(ablate & 8192)) {            // (diagnostic 8192: no min / max atomics)
+                if (mn < mm[i].x) atomicMin(&T.w[sl][22], mn);
+                if (mx > mm[i].y) atomicMax(&T.w[sl][23], mx);
+            }
             if (AFF && nnf) atomicOr(&T.w[sl][21], ADJ_FLAG);
-            atomicAdd(&T.sum[sl], sm);
-            atomicAdd(&T.sq[sl], sq);
+            if (!(ablate & 4096)) {            // (diagnostic 4096: no f64 sum atomics)
+                atomicAdd(&T.sum[sl], sm);
+                atomicAdd(&T.sq[sl], sq);
+            }
         }
     }
 }
@@ -618,18 +624,32 @@ __device__ __forceinline__ void fold_batch(Table& T, const StageT* __restrict__ 
         if (MODE != MODE_GRAPH && slot[i] >= 0)
             pv[i] = __hip_atomic_load(&T.w[slot[i]][24], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
+    // ... and their ordered min / max, in the same round trip: the min / max
+    // atomics are issued only by lanes whose values extend the entry's range
+    // (values only move outward, so a stale read can only ask for an atomic
+    // that changes nothing, never skip one that would).  Unconditional, they
+    // were ~1/3 of the 2048^3 scan's LDS bank-conflict cycles.
+    uint2 mm[NPER];
+#pragma unroll
+    for (int i = 0; i < NPER; ++i) {
+        mm[i] = make_uint2(ORD_POS_INF, ORD_NEG_INF);
+        if (MODE != MODE_GRAPH && slot[i] >= 0)
+            mm[i] = make_uint2(__hip_atomic_load(&T.w[slot[i]][22], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP),
+                               __hip_atomic_load(&T.w[slot[i]][23], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+    }
 #if CTG_PAIR_FOLD
     // grouped atomics: whole-array boundary maps and nearest-neighbour
     // affinity faces (single-sample entries)
     if constexpr ((MODE == MODE_BOUNDARY || MODE == MODE_AFF_NN) && !BATCH) {
-        fold_grouped<MODE, FAST40, BATCH, StageT, NPER>(T, e, slot, pv, lane, R, C, scale, offset, ablate);
+        fold_grouped<MODE, FAST40, BATCH, StageT, NPER>(T, e, slot, pv, mm, lane, R, C, scale, offset, ablate);
         return;
     }
 #endif
 #pragma unroll
     for (int i = 0; i < NPER; ++i)
         if (slot[i] != -2)
-            fold_stats<MODE, FAST40, BATCH, StageT>(T, e[i], slot[i], pv[i], R, C, scale, offset, need, ablate);
+            fold_stats<MODE, FAST40, BATCH, StageT>(T, e[i], slot[i], pv[i], mm[i], R, C, scale, offset, need,
+                                                    ablate);
 }
 
 // diagnostic time stamp (volatile: never merged or moved across other code)
