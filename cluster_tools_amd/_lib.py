@@ -23,6 +23,8 @@ CTG_DATA_U8 = 2
 CTG_KEEP_STATS = 1
 CTG_NO_ADJ_FILTER = 2
 CTG_NO_NODES = 4
+CTG_DEFER_STATS = 8
+CTG_ERR_STALE = -5
 CTG_MAX_CHANNELS = 24
 CTG_N_FEATURES = 10
 CTG_NBINS = 40

@@ -200,6 +200,7 @@ static void free_records(Workspace& w) {
 }
 
 hipError_t ensure_records(Workspace& w, int64_t need, int wide) {
+    ++w.gen;   // a scan is about to overwrite the records
     if (need <= w.rec.cap && w.rec.key) return hipSuccess;
     free_records(w);
     const int words = wide ? WREC_WORDS : NREC_STRIDE;
@@ -312,6 +313,7 @@ struct ReduceJob {
     int ub = 0;                        // bits of the key's u field (0: = bits of the largest label)
     uint64_t umask = ~0ull;            // label bits of u (batched blocks: below the block tag)
     int skip_nodes = 0;                // batched blocks: nodes come from the per-block unique pass
+    int defer_stats = 0;               // CTG_DEFER_STATS (with keep_stats)
 };
 
 static hipError_t reduce_records(Workspace& w, const ReduceJob& J, hipStream_t s, ctg_result* res) {
@@ -321,6 +323,7 @@ static hipError_t reduce_records(Workspace& w, const ReduceJob& J, hipStream_t s
     // the record count n (an upper bound), so the back half issues no
     // host synchronisation (except on the rare node path for labels >= 2^30).
     Ev ev{w, s};
+    ++w.gen;   // the sort / run buffers are about to be overwritten
     const int64_t n = J.n;
     const int nb = bits_for(J.max_v);
     const int ub = J.ub ? J.ub : nb;
@@ -440,11 +443,14 @@ static hipError_t reduce_records(Workspace& w, const ReduceJob& J, hipStream_t s
 
     // outputs (uncompacted), sized by the bound n
     const bool may_drop = J.need_adj || J.ignore_label;
+    // CTG_DEFER_STATS: result row e is run e of the records (no compaction),
+    // whose statistics the exchange rebuilds where it needs them
+    const bool defer = J.defer_stats && J.keep_stats && J.stats && !J.wide && !may_drop;
     ReduceOut O{};
     O.edges = (uint64_t*)dalloc(n * 16);
     O.feats = J.stats ? (double*)dalloc(n * N_FEATURES * 8) : nullptr;
     O.keep = may_drop ? w.keep : nullptr;
-    if (J.keep_stats && J.stats) {
+    if (J.keep_stats && J.stats && !defer) {
         O.wstats = (uint32_t*)dalloc(n * WREC_WORDS * 4);
         O.wsums = (double2*)dalloc(n * 16);
     }
@@ -480,6 +486,14 @@ static hipError_t reduce_records(Workspace& w, const ReduceJob& J, hipStream_t s
     res->edges = O.edges;
     res->features = O.feats;
     res->stats = O.wstats;
+    if (defer) {
+        res->defer.on = 1;
+        res->defer.offs = w.offs;
+        res->defer.runs = w.runs;
+        res->defer.perm = Perm{packed ? nullptr : w.idx_out, packed ? w.sk_out : nullptr, packed ? ib : 0};
+        res->defer.hist = J.R.hist;
+        res->defer.gen = w.gen;
+    }
     res->stat_sums = O.wsums;
 
     // nodes = unique endpoints of every unique key (before filtering)
@@ -642,9 +656,13 @@ int ctg_mgpu_pack(const ctg_result* local, const int64_t* counts_all, int world_
         set_error("ctg_mgpu_pack: counts do not cover this rank's table");
         return CTG_ERR_ARG;
     }
-    if (words > 0 && (!send || !local->stats || !local->stat_sums)) {
+    if (words > 0 && (!send || (!(local->stats && local->stat_sums) && !local->defer.on))) {
         set_error("ctg_mgpu_pack: rows to send need a CTG_KEEP_STATS table and a send buffer");
         return CTG_ERR_ARG;
+    }
+    if (words > 0 && local->defer.on && local->defer.gen != ws(local->device).gen) {
+        set_error("ctg_mgpu_pack: the CTG_DEFER_STATS table's records were overwritten by a later call");
+        return CTG_ERR_STALE;
     }
     CTG_CHECK(mgpu_pack(local, counts_all, world_size, rank, send, (hipStream_t)stream));
     return CTG_OK;
@@ -676,6 +694,10 @@ int ctg_mgpu_merge(ctg_result* local, const int64_t* recv, const int64_t* counts
     if (recv_words > 0 && !recv) {
         set_error("ctg_mgpu_merge: null receive buffer");
         return CTG_ERR_ARG;
+    }
+    if (recv_words > 0 && local->defer.on && local->defer.gen != ws(local->device).gen) {
+        set_error("ctg_mgpu_merge: the CTG_DEFER_STATS table's records were overwritten by a later call");
+        return CTG_ERR_STALE;
     }
     Workspace& w = ws(cur_dev());
     CTG_CHECK(ws_init(w));
@@ -1195,6 +1217,7 @@ int ctg_rag_features(const void* labels, int label_bits, const void* data, int d
     if (P.bloom) J.need_adj = 1;   // drop the Bloom filter's false positives
     J.ignore_label = ignore_label;
     J.keep_stats = (flags & CTG_KEEP_STATS) ? 1 : 0;
+    J.defer_stats = (flags & CTG_DEFER_STATS) ? 1 : 0;
     J.max_v = w.counters_host->max_v;
     J.scale = P.scale;
     J.offset = P.offset;

@@ -202,6 +202,30 @@ struct Counters {               // device-side counters, zeroed per call
     unsigned long long rcount[NREG];  // records reserved per region (may exceed rcap: overflow)
 };
 
+// record slot of sorted position r: a u32 index array, or the low ib bits of
+// the packed sort keys (keys-only record sort, no unpack pass)
+struct Perm {
+    const uint32_t* p32;
+    const uint64_t* p64;
+    int ib;
+    __device__ __forceinline__ uint32_t operator()(uint32_t r) const {
+        return p64 ? (uint32_t)(p64[r] & ((1ull << ib) - 1ull)) : p32[r];
+    }
+};
+
+// CTG_DEFER_STATS: what a result needs to rebuild an edge's mergeable
+// statistics from its records -- run e of the sorted records is slots
+// perm(offs[e] .. offs[e] + runs[e]) of the narrow record bodies `hist` --
+// valid while the workspace's generation is still `gen`
+struct DeferredStats {
+    int on = 0;
+    const uint32_t* offs = nullptr;
+    const uint32_t* runs = nullptr;
+    Perm perm{nullptr, nullptr, 0};
+    const uint32_t* hist = nullptr;
+    uint64_t gen = 0;
+};
+
 struct ReduceOut {
     uint64_t* edges;      // 2E
     double* feats;        // 10E or null
@@ -217,6 +241,9 @@ constexpr int GS_SMALL_WORDS = 5 * 65536 + 8;    // group sort: counts, offsets,
 
 struct Workspace {
     int device = -1;
+    // bumped by every call that overwrites the records or the sort / run
+    // buffers (a CTG_DEFER_STATS handle compares it)
+    uint64_t gen = 1;
     RecordBuf rec;
     // sort / reduce scratch
     uint64_t* sk_in = nullptr; uint64_t* sk_out = nullptr;
@@ -274,6 +301,8 @@ struct ctg_result {
     // affinity partial table (CTG_NO_ADJ_FILTER): a key is an edge only where
     // some record carries the ADJ bit (decided after a merge)
     int partial_adj = 0;
+    // CTG_DEFER_STATS: statistics rows rebuilt from the records on demand
+    ctg::DeferredStats defer;
     // allocations this handle frees instead of the five pointers above, which
     // then point into them (a multi-GPU shard that is a range of its rank's
     // local table: ctg_mgpu_merge)

@@ -148,6 +148,7 @@ __global__ void k_mgpu_pack(Segs S, const uint64_t* __restrict__ edges, const do
             const int64_t r = S.e_start[s] + off / ROW;
             const int w = (int)(off % ROW);
             if (w < 2) val = edges[2 * r + w];
+            else if (!wide64) continue;   // CTG_DEFER_STATS: k_mgpu_pack_deferred writes the statistics
             else if (w < 4) {
                 const double2 sm = sums[r];
                 val = (uint64_t)__double_as_longlong(w == 2 ? sm.x : sm.y);
@@ -159,6 +160,31 @@ __global__ void k_mgpu_pack(Segs S, const uint64_t* __restrict__ edges, const do
         }
         out[i] = val;
     }
+}
+
+// CTG_DEFER_STATS: one thread per row to send -- its statistics rebuilt from
+// its records (words 2..27 of the row; k_mgpu_pack writes the key words).
+// Boundary maps only: every key is an edge (the reduce's need_adj 0 sets ADJ).
+__global__ __launch_bounds__(256) void k_mgpu_pack_deferred(Segs S, DeferredStats D, uint64_t* __restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    int s = 0;
+    int64_t before = 0;
+    while (s < S.n && i >= before + S.e_cnt[s]) before += S.e_cnt[s++];
+    if (s >= S.n) return;
+    const int64_t a = i - before, r = S.e_start[s] + a;
+    uint32_t h[NSLOTS];
+#pragma unroll
+    for (int j = 0; j < NSLOTS; ++j) h[j] = 0;
+    uint32_t cnt = 0, flags = ADJ_FLAG, mn = ORD_POS_INF, mx = ORD_NEG_INF;
+    Moments mo;
+    edge_from_records(D, r, h, cnt, flags, mn, mx, mo);
+    uint32_t w[WREC_WORDS];
+    wide_row(h, cnt, flags, mn, mx, mo, w);
+    uint64_t* o = out + S.w_off[s] + a * ROW;
+    o[2] = (uint64_t)__double_as_longlong(mo.S1);
+    o[3] = (uint64_t)__double_as_longlong(mo.S2);
+#pragma unroll
+    for (int t = 0; t < WREC_WORDS / 2; ++t) o[4 + t] = (uint64_t)w[2 * t] | ((uint64_t)w[2 * t + 1] << 32);
 }
 
 // ---------------------------------------------------------------------------
@@ -250,6 +276,8 @@ struct MergeIO {
     const double* own_feats;
     const uint32_t* own_wide;
     const double2* own_sums;
+    DeferredStats defer;  // on: own rows' statistics from the records (own row i = run own_row0 + i)
+    int64_t own_row0;
     int64_t n_own;
     // received rows, sorted order and runs
     const uint64_t* recv;
@@ -284,7 +312,11 @@ __global__ __launch_bounds__(256) void k_mgpu_combine(RecvSegs S, MergeIO io) {
     uint32_t cnt = 0, flags = 0, mn = ORD_POS_INF, mx = ORD_NEG_INF;
     Moments mo;
     uint32_t w[WREC_WORDS];
-    if (found) {
+    if (found && io.defer.on) {   // the own row's records (boundary maps: every key an edge)
+        flags = ADJ_FLAG;
+        edge_from_records(io.defer, io.own_row0 + ins, h, cnt, flags, mn, mx, mo);
+        io.touched[ins] = (uint32_t)k + 1u;
+    } else if (found) {
         const uint4* q = reinterpret_cast<const uint4*>(io.own_wide + ins * WREC_WORDS);
 #pragma unroll
         for (int j = 0; j < WREC_WORDS / 4; ++j) {
@@ -437,9 +469,18 @@ hipError_t mgpu_pack(const ctg_result* r, const int64_t* counts_all, int world, 
     }
     S.w_off[S.n] = w;
     if (w == 0) return hipSuccess;
+    const bool defer = r->defer.on && !r->stats;
     const int64_t blocks = std::min<int64_t>((w + 255) / 256, 8192);
     hipLaunchKernelGGL(k_mgpu_pack, dim3((unsigned)blocks), dim3(256), 0, s, S, r->edges, r->stat_sums,
-                       reinterpret_cast<const uint64_t*>(r->stats), r->nodes, reinterpret_cast<uint64_t*>(send));
+                       defer ? nullptr : reinterpret_cast<const uint64_t*>(r->stats), r->nodes,
+                       reinterpret_cast<uint64_t*>(send));
+    if (defer) {
+        int64_t rows = 0;
+        for (int i = 0; i < S.n; ++i) rows += S.e_cnt[i];
+        if (rows > 0)
+            hipLaunchKernelGGL(k_mgpu_pack_deferred, dim3((unsigned)((rows + 255) / 256)), dim3(256), 0, s, S,
+                               r->defer, reinterpret_cast<uint64_t*>(send));
+    }
     return hipGetLastError();
 }
 
@@ -548,7 +589,8 @@ hipError_t mgpu_merge(ctg_result* L, const int64_t* recv, const int64_t* counts_
         L->features = nullptr;
         return hipSuccess;
     }
-    if (!L->stats || !L->features) return hipErrorInvalidValue;   // needs a CTG_KEEP_STATS partial table
+    // needs a CTG_KEEP_STATS partial table (rows, or CTG_DEFER_STATS records)
+    if ((!L->stats && !L->defer.on) || !L->features) return hipErrorInvalidValue;
     // row indices, run heads and output positions below are u32
     if (M >= (1ll << 32) || e_cnt + M >= (1ll << 32) || NM >= (1ll << 32)) {
         set_error("ctg_mgpu_merge: more than 2^32 rows in one shard (split the slab over more ranks)");
@@ -558,8 +600,10 @@ hipError_t mgpu_merge(ctg_result* L, const int64_t* recv, const int64_t* counts_
     MergeIO io{};
     io.own_edges = L->edges + 2 * e_lo;
     io.own_feats = L->features + 10 * e_lo;
-    io.own_wide = L->stats + WREC_WORDS * e_lo;
-    io.own_sums = L->stat_sums + e_lo;
+    io.own_wide = L->stats ? L->stats + WREC_WORDS * e_lo : nullptr;
+    io.own_sums = L->stat_sums ? L->stat_sums + e_lo : nullptr;
+    if (!L->stats) io.defer = L->defer;
+    io.own_row0 = e_lo;
     io.n_own = e_cnt;
     io.recv = rv;
     io.partial_adj = L->partial_adj;

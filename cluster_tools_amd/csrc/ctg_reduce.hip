@@ -69,30 +69,6 @@ __global__ void k_max_pairs(int64_t n, const uint64_t* __restrict__ uv, unsigned
     if ((threadIdx.x & 63) == 0 && m) atomicMax(out, m);
 }
 
-// one narrow 128-byte record body at p: (S1, S2), the 24 record words, the pivot
-__device__ __forceinline__ void add_narrow(const uint4* p, uint32_t (&h)[NSLOTS], uint32_t& cnt, uint32_t& flags,
-                                           uint32_t& mn, uint32_t& mx, Moments& mo) {
-    const double2 sw = *reinterpret_cast<const double2*>(p);
-    uint32_t w[NREC_WORDS];
-#pragma unroll
-    for (int j = 0; j < NREC_WORDS / 4; ++j) {
-        uint4 v = p[1 + j];
-        w[4 * j] = v.x; w[4 * j + 1] = v.y; w[4 * j + 2] = v.z; w[4 * j + 3] = v.w;
-    }
-    const uint32_t piv = p[7].x;
-#pragma unroll
-    for (int j = 0; j < HWORDS; ++j) {
-        h[2 * j] += w[j] & 0xFFFFu;
-        h[2 * j + 1] += w[j] >> 16;
-    }
-    const uint32_t n = w[21] & ~ADJ_FLAG;
-    cnt += n;
-    flags |= w[21] & ADJ_FLAG;
-    mn = min(mn, w[22]);
-    mx = max(mx, w[23]);
-    mo.add(n, sw.x, sw.y, piv);
-}
-
 template <bool WIDE>
 __device__ __forceinline__ void load_record(const RecordBuf& R, uint32_t i, uint32_t (&h)[NSLOTS], uint32_t& cnt,
                                             uint32_t& flags, uint32_t& mn, uint32_t& mx, Moments& mo) {
@@ -111,17 +87,6 @@ __device__ __forceinline__ void load_record(const RecordBuf& R, uint32_t i, uint
     }
 }
 
-// record slot of sorted position r: a u32 index array, or the low ib bits of
-// the packed sort keys (keys-only record sort, no unpack pass)
-struct Perm {
-    const uint32_t* p32;
-    const uint64_t* p64;
-    int ib;
-    __device__ __forceinline__ uint32_t operator()(uint32_t r) const {
-        return p64 ? (uint32_t)(p64[r] & ((1ull << ib) - 1ull)) : p32[r];
-    }
-};
-
 // per-edge epilogue of the reduce: keep flag, mergeable stats row; the feature
 // row is returned in registers (k_reduce_edges stages it for coalesced stores)
 __device__ __forceinline__ void reduce_epilogue(int64_t e, uint64_t u, uint32_t (&h)[NSLOTS], uint32_t cnt,
@@ -137,13 +102,7 @@ __device__ __forceinline__ void reduce_epilogue(int64_t e, uint64_t u, uint32_t 
     if (O.wstats) {
         uint4* p = (uint4*)(O.wstats + (size_t)e * WREC_WORDS);
         uint32_t w[WREC_WORDS];
-#pragma unroll
-        for (int j = 0; j < NSLOTS; ++j) w[j] = h[j];
-        w[42] = cnt | (flags & ADJ_FLAG);
-        w[43] = mn;
-        w[44] = mx;
-        w[WREC_PIV] = __float_as_uint((float)mo.p0);   // a sample: exact in f32
-        w[46] = w[47] = 0;
+        wide_row(h, cnt, flags, mn, mx, mo, w);
 #pragma unroll
         for (int j = 0; j < WREC_WORDS / 4; ++j) p[j] = make_uint4(w[4 * j], w[4 * j + 1], w[4 * j + 2], w[4 * j + 3]);
         O.wsums[e] = make_double2(sum, sq);

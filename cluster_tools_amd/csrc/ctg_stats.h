@@ -166,6 +166,55 @@ struct Moments {
     }
 };
 
+// one narrow 128-byte record body at p: (S1, S2), the 24 record words, the pivot
+__device__ __forceinline__ void add_narrow(const uint4* p, uint32_t (&h)[NSLOTS], uint32_t& cnt, uint32_t& flags,
+                                           uint32_t& mn, uint32_t& mx, Moments& mo) {
+    const double2 sw = *reinterpret_cast<const double2*>(p);
+    uint32_t w[NREC_WORDS];
+#pragma unroll
+    for (int j = 0; j < NREC_WORDS / 4; ++j) {
+        uint4 v = p[1 + j];
+        w[4 * j] = v.x; w[4 * j + 1] = v.y; w[4 * j + 2] = v.z; w[4 * j + 3] = v.w;
+    }
+    const uint32_t piv = p[7].x;
+#pragma unroll
+    for (int j = 0; j < HWORDS; ++j) {
+        h[2 * j] += w[j] & 0xFFFFu;
+        h[2 * j + 1] += w[j] >> 16;
+    }
+    const uint32_t n = w[21] & ~ADJ_FLAG;
+    cnt += n;
+    flags |= w[21] & ADJ_FLAG;
+    mn = min(mn, w[22]);
+    mx = max(mx, w[23]);
+    mo.add(n, sw.x, sw.y, piv);
+}
+
+// An edge's combined statistics from its run e of sorted narrow records (the
+// reduce's accumulation, k_reduce_edges): CTG_DEFER_STATS rows on demand.
+__device__ __forceinline__ void edge_from_records(const DeferredStats& D, int64_t e, uint32_t (&h)[NSLOTS],
+                                                  uint32_t& cnt, uint32_t& flags, uint32_t& mn, uint32_t& mx,
+                                                  Moments& mo) {
+    const uint32_t b = D.offs[e], n = D.runs[e];
+    for (uint32_t r = b; r < b + n; ++r)
+        add_narrow(reinterpret_cast<const uint4*>(D.hist + (size_t)D.perm(r) * NREC_STRIDE), h, cnt, flags, mn, mx,
+                   mo);
+}
+
+// the mergeable wide statistics record of an edge (48 words: 42 slots,
+// count | ADJ, ordered min, ordered max, pivot bits, pad); its (S1, S2) are
+// mo.S1 / mo.S2 about the pivot mo.p0
+__device__ __forceinline__ void wide_row(const uint32_t (&h)[NSLOTS], uint32_t cnt, uint32_t flags, uint32_t mn,
+                                         uint32_t mx, const Moments& mo, uint32_t (&w)[WREC_WORDS]) {
+#pragma unroll
+    for (int j = 0; j < NSLOTS; ++j) w[j] = h[j];
+    w[42] = cnt | (flags & ADJ_FLAG);
+    w[43] = mn;
+    w[44] = mx;
+    w[WREC_PIV] = __float_as_uint((float)mo.p0);   // a sample: exact in f32
+    w[46] = w[47] = 0;
+}
+
 // The 10 feature columns of one edge from its combined statistics (count, the
 // 42-slot histogram, ordered min / max, shifted sums about mo.p0) as five
 // column pairs in registers; an edge without samples gets a zero row.

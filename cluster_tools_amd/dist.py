@@ -62,7 +62,16 @@ def _stream():
 
 
 class HipBackend:
-    """The device steps of the exchange through libctg.so (ctg_mgpu_*)."""
+    """The device steps of the exchange through libctg.so (ctg_mgpu_*).
+
+    defer_stats (default): the local call writes no mergeable-statistics rows;
+    ctg_mgpu_pack / ctg_mgpu_merge rebuild them from the call's records only
+    for the rows that leave the rank and the own rows that meet a received key
+    (CTG_DEFER_STATS; boundary maps without ignore_label -- the library writes
+    the rows for every other call).  False: every row is written (CTG_KEEP_STATS)."""
+
+    def __init__(self, defer_stats=True):
+        self.defer_stats = defer_stats
 
     def local(self, labels, data, offsets, own_begin, own_end, ignore_label, hist_range):
         """This rank's partial table: a device-resident rag.Result with the
@@ -71,7 +80,7 @@ class HipBackend:
         from . import rag
         return rag.rag_features_handle(labels, data, offsets=offsets, own_begin=own_begin, own_end=own_end,
                                        ignore_label=ignore_label, hist_range=hist_range, keep_stats=True,
-                                       no_adj_filter=offsets is not None)
+                                       no_adj_filter=offsets is not None, defer_stats=self.defer_stats)
 
     def sample(self, loc):
         meta = torch.empty(N_SAMPLES + 1, dtype=torch.int64, device='cuda')

@@ -141,14 +141,18 @@ def _check_offsets(offsets):
 
 
 def rag_features_handle(labels, data=None, offsets=None, own_begin=None, own_end=None, ignore_label=False,
-                        hist_range=(0.0, 1.0), keep_stats=False, stream=None, no_adj_filter=False):
+                        hist_range=(0.0, 1.0), keep_stats=False, stream=None, no_adj_filter=False,
+                        defer_stats=False):
     """Run the hot path and return the device-resident ``Result`` handle.
 
     labels: (Z,Y,X) uint64/uint32 numpy array or CUDA tensor (int64/int32 views
     of unsigned labels are accepted for torch); data: None, (Z,Y,X) boundary
     map or (C,Z,Y,X) affinities (float32 or uint8); offsets: C x 3 for
     affinities.  keep_stats keeps the mergeable wide records; no_adj_filter
-    (affinities) keeps sampled pairs that are not edges of this array's RAG.
+    (affinities) keeps sampled pairs that are not edges of this array's RAG;
+    defer_stats (with keep_stats, for the multi-GPU exchange only:
+    CTG_DEFER_STATS) writes no statistics rows -- the exchange rebuilds the
+    rows it needs from this call's records, valid until the next call.
     """
     lib = L.load()
     dev = L.init_device()
@@ -195,7 +199,8 @@ def rag_features_handle(labels, data=None, offsets=None, own_begin=None, own_end
     else:
         if tuple(data.shape) != tuple(shape):
             raise ValueError('boundary map shape %s != labels shape %s' % (tuple(data.shape), tuple(shape)))
-    flags = (L.CTG_KEEP_STATS if keep_stats else 0) | (L.CTG_NO_ADJ_FILTER if no_adj_filter else 0)
+    flags = ((L.CTG_KEEP_STATS if keep_stats else 0) | (L.CTG_NO_ADJ_FILTER if no_adj_filter else 0) |
+             (L.CTG_DEFER_STATS if keep_stats and defer_stats else 0))
     sh = _shape_arr(shape)
     ob = _shape_arr(own_begin) if own_begin is not None else None
     oe = _shape_arr(own_end) if own_end is not None else None

@@ -48,6 +48,7 @@ extern "C" {
 #define CTG_ERR_HIP -2
 #define CTG_ERR_NOMEM -3
 #define CTG_ERR_UNSUPPORTED -4
+#define CTG_ERR_STALE -5   /* a CTG_DEFER_STATS handle whose records were overwritten by a later call */
 
 #define CTG_MEM_HOST 0
 #define CTG_MEM_DEVICE 1
@@ -62,6 +63,15 @@ extern "C" {
 #define CTG_NO_ADJ_FILTER 2   /* affinities: keep sample pairs that are not nearest-neighbour
                                  edges of this array (their records carry no ADJ bit); the
                                  caller filters after a merge or by an edge list */
+#define CTG_DEFER_STATS 8     /* with CTG_KEEP_STATS, for the ctg_mgpu_* exchange: no statistics
+                                 rows are written; ctg_mgpu_pack / ctg_mgpu_merge rebuild a row's
+                                 statistics from the call's records where the exchange needs them
+                                 (rows sent to another rank, own rows that meet a received key).
+                                 The records stay in the device's workspace, so the handle serves
+                                 ctg_mgpu_pack / ctg_mgpu_merge only until the next ctg_rag_* or
+                                 ctg_merge_stats call on that device (then CTG_ERR_STALE), and
+                                 ctg_result_copy_stats has no rows to copy.  Boundary maps without
+                                 ignore_label; any other call writes the CTG_KEEP_STATS rows. */
 
 #define CTG_MAX_CHANNELS 24
 #define CTG_N_FEATURES 10

@@ -413,19 +413,45 @@ def test_unique_and_map_helpers(gpu):
     np.testing.assert_array_equal(rag.unique_labels(lab, (2, 3, 4), (7, 9, 10)), np.unique(lab[2:7, 3:9, 4:10]))
 
 
-def test_hip_backend_slabs_merge(gpu):
+@pytest.mark.parametrize('defer', [False, True])
+def test_hip_backend_slabs_merge(gpu, defer):
     """The multi-GPU data path (local partials -> ctg_mgpu_split / pack ->
     exchanged rows -> ctg_mgpu_merge) for 2 and 3 z-slabs on one GPU
-    (tests/exchange_sim.py) == the oracle's whole-volume features."""
+    (tests/exchange_sim.py) == the oracle's whole-volume features; with the
+    statistics rows written by the local calls (CTG_KEEP_STATS) and rebuilt
+    from the records by the exchange (CTG_DEFER_STATS) -- the two agree to
+    the f64 summation order (record slots come from the scan's flush atomics,
+    so two calls may sum an edge's records in a different order)."""
     from cluster_tools_amd import dist as cdist
     from tests.exchange_sim import simulate
     shape = (40, 48, 56)
     lab, bnd = rag.synth_volume(shape, cell=6, seed=21)
     e_ref, f_ref = O.boundary_features(lab.cpu().numpy().view(np.uint64), bnd.cpu().numpy())
     for world in (2, 3):
-        shards = simulate(cdist.HipBackend(), lab, bnd, world)
-        np.testing.assert_array_equal(np.concatenate([x.edges() for x in shards]), e_ref)
-        check_features(np.concatenate([x.features() for x in shards]), f_ref)
+        shards = simulate(cdist.HipBackend(defer_stats=defer), lab, bnd, world, fresh=defer)
+        e = np.concatenate([x.edges() for x in shards])
+        f = np.concatenate([x.features() for x in shards])
+        np.testing.assert_array_equal(e, e_ref)
+        check_features(f, f_ref)
+        if defer:
+            eager = simulate(cdist.HipBackend(defer_stats=False), lab, bnd, world)
+            np.testing.assert_array_equal(np.concatenate([x.edges() for x in eager]), e)
+            np.testing.assert_allclose(np.concatenate([x.features() for x in eager]), f, rtol=1e-12, atol=1e-15)
+
+
+def test_deferred_stats_stale_after_another_call(gpu):
+    """A CTG_DEFER_STATS table serves ctg_mgpu_pack only while its records are
+    the device's latest: after another call, pack refuses it (CTG_ERR_STALE)
+    instead of reading overwritten records; a rank with nothing to send or
+    receive never needs them."""
+    from cluster_tools_amd import _lib
+    from cluster_tools_amd import dist as cdist
+    from tests.exchange_sim import simulate
+    lab, bnd = rag.synth_volume((40, 48, 56), cell=6, seed=21)
+    with pytest.raises(_lib.CtgError, match='overwritten'):
+        simulate(cdist.HipBackend(defer_stats=True), lab, bnd, 2)
+    shards = simulate(cdist.HipBackend(defer_stats=True), lab, bnd, 1)   # world 1: no rows move
+    assert shards[0].n_edges > 0
 
 
 def test_hip_backend_affinity_slabs_merge(gpu):
@@ -440,6 +466,7 @@ def test_hip_backend_affinity_slabs_merge(gpu):
     affs = rag.synth_affinities(bnd, offs)
     e_ref, f_ref = O.affinity_features(lab.cpu().numpy().view(np.uint64), affs.cpu().numpy(), offs)
     for world in (2, 3):
+        # (long-range partials keep the written rows: CTG_DEFER_STATS falls back)
         shards = simulate(cdist.HipBackend(), lab, affs, world, offsets=offs)
         np.testing.assert_array_equal(np.concatenate([x.edges() for x in shards]), e_ref)
         check_features(np.concatenate([x.features() for x in shards]), f_ref)
