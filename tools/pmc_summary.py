@@ -36,13 +36,17 @@ def kernel_stats(d):
 
 
 def counter_per_dispatch(d, counter):
+    """Median over a kernel's dispatches: the first call of a fresh process
+    may overflow its initially sized record buffer and rescan (a launch that
+    drops the records past the capacity -- at configs[4] it wrote 6.2 of
+    17.9 GB), and a mean would count that partial launch in."""
     acc = {}
     for r in _rows(os.path.join(d, '**', '*counter_collection.csv')):
         if r.get('Counter_Name') != counter:
             continue
         name = r.get('Kernel_Name', '')
         acc.setdefault(name, []).append(float(r['Counter_Value']))
-    return {k: sum(v) / len(v) for k, v in acc.items()}
+    return {k: sorted(v)[len(v) // 2] for k, v in acc.items()}
 
 
 def pick(d, sub):
@@ -89,7 +93,8 @@ def main():
         'read_factor': rfac,
         'write_factor': wfac,
         'factor_source': fsrc,
-        'note': 'HBM bytes = read_factor x FETCH_SIZE x 1024 + write_factor x WRITE_SIZE x 1024',
+        'note': 'HBM bytes = read_factor x FETCH_SIZE x 1024 + write_factor x WRITE_SIZE x 1024 '
+                '(per-dispatch medians)',
         'git_sha': sha,
     }
     # the face scan's average duration from the kernel trace (the launched
