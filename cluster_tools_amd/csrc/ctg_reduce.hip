@@ -312,7 +312,9 @@ __global__ __launch_bounds__(256) void k_mark_nodes_win(int64_t E, const uint32_
         // u is sorted: only a run head marks it (the previous key is the
         // previous lane's, or a reload for the wave's first lane)
         uint32_t up = (uint32_t)__shfl_up((int)u, 1, 64);
-        if (lane == 0) up = e > 0 ? (uint32_t)(uniq[e - 1] >> nb) : ~u;
+        // (only lanes holding an edge: past e1 the index can leave uniq's
+        // allocation, which is sized by this call's records)
+        if (lane == 0 && e < e1) up = e > 0 ? (uint32_t)(uniq[e - 1] >> nb) : ~u;
         if (e < e1) {
             if (win) {
                 if (up != u) atomicOr(&bm[(u - base) >> 5], 1u << ((u - base) & 31));

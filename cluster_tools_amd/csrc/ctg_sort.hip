@@ -367,6 +367,38 @@ struct GsParams {
 
 __device__ __forceinline__ uint64_t gs_packed(uint64_t k, int nb) { return ((k >> 32) << nb) | (k & 0xFFFFFFFFull); }
 
+// The workgroup's bucket range [lo, hi] (hi < lo: no item).  A region chunk's
+// records were flushed by tiles scanned at about the same time, so they span a
+// few hundred of the (up to 64 K) buckets: the counter passes below zero, count
+// and reserve only that window instead of every bucket.
+__device__ __forceinline__ void gs_bucket_range(const uint32_t (&bk)[GS_IPT], uint32_t* red, uint32_t& lo,
+                                                uint32_t& hi) {
+    uint32_t mn = 0xFFFFFFFFu, mx = 0u;
+#pragma unroll
+    for (int q = 0; q < GS_IPT; ++q) {
+        if (bk[q] != 0xFFFFFFFFu) {
+            mn = min(mn, bk[q]);
+            mx = max(mx, bk[q]);
+        }
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        mn = min(mn, (uint32_t)__shfl_xor((int)mn, o, 64));
+        mx = max(mx, (uint32_t)__shfl_xor((int)mx, o, 64));
+    }
+    if (threadIdx.x == 0) {
+        red[0] = 0xFFFFFFFFu;
+        red[1] = 0u;
+    }
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) {
+        atomicMin(&red[0], mn);
+        atomicMax(&red[1], mx);
+    }
+    __syncthreads();
+    lo = red[0];
+    hi = red[1];
+}
+
 __global__ __launch_bounds__(GS_PASS_THREADS) void k_gs_hist(GsParams P, uint32_t* __restrict__ counts) {
     extern __shared__ uint32_t h[];   // min(nbk, GS_HALF) counters
     const int r = blockIdx.y;
@@ -380,10 +412,15 @@ __global__ __launch_bounds__(GS_PASS_THREADS) void k_gs_hist(GsParams P, uint32_
     for (int q = 0; q < GS_IPT; ++q) {
         const uint32_t j = c0 + q * GS_PASS_THREADS + threadIdx.x;
         const uint64_t k = src[min(j, cnt - 1)];
-        bk[q] = j < cnt ? (uint32_t)(gs_packed(k, P.nb) >> P.shift) : 0xFFFFFFFFu;
+        const uint32_t b = (uint32_t)(gs_packed(k, P.nb) >> P.shift);
+        bk[q] = j < cnt && b < P.nbk ? b : 0xFFFFFFFFu;   // (the bucket loop's bound, as before the window)
     }
-    for (uint32_t h0 = 0; h0 < P.nbk; h0 += GS_HALF) {   // 64 K buckets: two passes over 128 KB of counters
-        const uint32_t hn = min(GS_HALF, P.nbk - h0);
+    __shared__ uint32_t red[2];
+    uint32_t lo, hi;
+    gs_bucket_range(bk, red, lo, hi);
+    // [lo, hi] in windows of at most GS_HALF counters (128 KB)
+    for (uint32_t h0 = lo; h0 <= hi && lo <= hi; h0 += GS_HALF) {
+        const uint32_t hn = min(GS_HALF, hi + 1 - h0);
         for (uint32_t i = threadIdx.x; i < hn; i += GS_PASS_THREADS) h[i] = 0;
         __syncthreads();
 #pragma unroll
@@ -467,11 +504,15 @@ __global__ __launch_bounds__(GS_PASS_THREADS) void k_gs_scatter(GsParams P, cons
     for (int q = 0; q < GS_IPT; ++q) {
         const uint32_t j = c0 + q * GS_PASS_THREADS + threadIdx.x;
         const uint64_t pk = gs_packed(it[q], P.nb);
-        bk[q] = j < cnt ? (uint32_t)(pk >> P.shift) : 0xFFFFFFFFu;
+        const uint32_t b = (uint32_t)(pk >> P.shift);
+        bk[q] = j < cnt && b < P.nbk ? b : 0xFFFFFFFFu;
         it[q] = ((pk & rmask) << P.ib) | ((uint64_t)r * (uint64_t)P.rcap + j);
     }
-    for (uint32_t h0 = 0; h0 < P.nbk; h0 += GS_HALF) {
-        const uint32_t hn = min(GS_HALF, P.nbk - h0);
+    __shared__ uint32_t red[2];
+    uint32_t lo, hi;
+    gs_bucket_range(bk, red, lo, hi);
+    for (uint32_t h0 = lo; h0 <= hi && lo <= hi; h0 += GS_HALF) {
+        const uint32_t hn = min(GS_HALF, hi + 1 - h0);
         for (uint32_t i = threadIdx.x; i < hn; i += GS_PASS_THREADS) h[i] = 0;
         __syncthreads();
 #pragma unroll

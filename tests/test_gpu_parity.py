@@ -94,6 +94,31 @@ def test_golden_boundary_f32(gpu, vol):
     check_features(out['features'], vol['bf_feats'])
 
 
+def test_fresh_process_small_calls(gpu):
+    """The first calls of a fresh process size the sort / run buffers to their
+    own record counts, so a kernel that reads past its valid range can leave
+    the allocation (a node-marking lane re-read the unique-key table past its
+    end; it faulted only when a small call came first in a process).  Small
+    calls of growing size, each checked against the golden volume's edges."""
+    import subprocess
+    import sys
+    code = (
+        "import numpy as np\n"
+        "from cluster_tools_amd import rag\n"
+        "z = np.load(%r)\n"
+        "for k in (1, 2, 3):\n"
+        "    lab = np.tile(z['bf_labels'], (k, k, 1))\n"
+        "    dat = np.tile(z['bf_data'], (k, k, 1))\n"
+        "    out = rag.rag_features(lab, dat)\n"
+        "    assert out['edges'].shape[0] > 0\n"
+        "out = rag.rag_features(z['bf_labels'], z['bf_data'])\n"
+        "assert (out['edges'] == z['bf_edges']).all()\n"
+        "print('FRESH_OK')\n") % os.path.join(GOLD, 'volumes.npz')
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, '-c', code], cwd=root, capture_output=True, text=True, timeout=180)
+    assert r.returncode == 0 and 'FRESH_OK' in r.stdout, r.stderr[-2000:]
+
+
 def test_golden_boundary_u8(gpu, vol):
     out = rag.rag_features(vol['bf_labels'], vol['bu_data'])
     np.testing.assert_array_equal(out['edges'], vol['bu_edges'])
