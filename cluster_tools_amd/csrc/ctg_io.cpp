@@ -500,8 +500,9 @@ ChunkPtr get_chunk(const std::string& path, int format, int ndim, const int64_t*
 // every n_jobs-th block (block_list[k::n_jobs], cluster_tasks.py), so the box
 // one stride past this one -- the stride being the step between this thread's
 // last two reads of the dataset -- and the next box in C order before a
-// stride is known.  A guess outside the chunk grid (the stride wrapping to the
-// next row) queues nothing.  CTG_IO_CACHE_MB=0 disables it.
+// stride is known -- and the kAhead boxes after it the same way.  A guess
+// outside the chunk grid (the stride wrapping to the next row) ends the
+// lookahead.  CTG_IO_CACHE_MB=0 disables it.
 // ---------------------------------------------------------------------------
 class Prefetcher {
 public:
@@ -554,6 +555,19 @@ private:
 };
 
 bool readahead_on() { return cache_budget() > 0; }   // (CTG_IO_CACHE_MB=0 turns both off)
+
+// boxes queued ahead of each read: a job walks one block per call, and one
+// block is one chunk per dataset here (a single gzip stream, decoded on one
+// thread), so one box of lookahead paces the job at one decode per call; the
+// next kAhead boxes keep the pool's threads busy on the blocks still to come
+constexpr int kAhead = 8;
+
+// a chunk already decoded or being decoded (no need to queue it)
+bool chunk_known(const std::string& path, int es, bool swap, int compression) {
+    const std::string key = path + "|" + std::to_string(es) + (swap ? "s" : "n") + std::to_string(compression);
+    std::lock_guard<std::mutex> g(g_cache_mu);
+    return g_cache.find(key) != g_cache.end();
+}
 
 // (dataset, thread) -> the chunk origin of that thread's previous box read
 struct LastBox {
@@ -718,10 +732,15 @@ int ctg_io_read_box(const char* ds_path, int format, int dtype_size, int big_end
             nxt[a] = c0[a];
             cnt[a] = nc[a];
         }
+        int64_t step[MAXD];
+        for (int a = 0; a < ndim; ++a) step[a] = 0;
         const bool strided = strided_next_box(ds_path, ndim, grid, c0, nxt);
-        if (strided ? nxt[0] >= 0 : next_chunk_box(ndim, grid, nxt, cnt)) {
-            const std::string ds(ds_path);
-            std::vector<int64_t> ch(chunks, chunks + ndim);
+        if (strided)
+            for (int a = 0; a < ndim; ++a) step[a] = nxt[a] - c0[a];
+        bool ok = strided ? nxt[0] >= 0 : next_chunk_box(ndim, grid, nxt, cnt);
+        const std::string ds(ds_path);
+        std::vector<int64_t> ch(chunks, chunks + ndim);
+        for (int k = 0; k < kAhead && ok; ++k) {
             for (int64_t ci = 0; ci < n_chunks; ++ci) {
                 int64_t pos[MAXD];
                 int64_t r = ci;
@@ -733,11 +752,21 @@ int ctg_io_read_box(const char* ds_path, int format, int dtype_size, int big_end
                 }
                 if (!inside) continue;
                 std::string path = chunk_path(ds.c_str(), format, ndim, pos);
+                if (chunk_known(path, es, swap, compression)) continue;
                 Prefetcher::get().submit([path, format, ndim, ch, es, swap, compression] {
                     bool missing = false;
                     std::string msg;
                     get_chunk(path, format, ndim, ch.data(), es, swap, compression, &missing, &msg);
                 });
+            }
+            // the box after: one more stride, or the next box in C order
+            if (strided) {
+                for (int a = 0; a < ndim; ++a) {
+                    nxt[a] += step[a];
+                    ok = ok && nxt[a] >= 0 && nxt[a] < grid[a];
+                }
+            } else {
+                ok = next_chunk_box(ndim, grid, nxt, cnt);
             }
         }
     }

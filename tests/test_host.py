@@ -413,15 +413,19 @@ def test_native_chunk_cache_sees_rewrites_and_threads(tmp_path, monkeypatch):
 
 def test_native_readahead_follows_the_job_stride(tmp_path, monkeypatch):
     """ADVICE r3 (low): a job walks every n_jobs-th block (block_list[k::n_jobs]),
-    so the readahead queues the box one stride past the last read (the step
-    between this thread's last two reads of the dataset), not the C-order
-    successor, which belongs to another job."""
+    so the readahead queues the boxes one stride, two strides, ... past the last
+    read (the step between this thread's last two reads of the dataset), not
+    the C-order successors, which belong to another job; it looks kAhead (8)
+    boxes ahead (one block = one gzip chunk decodes on one thread, so a single
+    box of lookahead paced a job at one decode per call), stops at the grid's
+    end and skips chunks already decoded or in flight."""
     import ctypes
     import time
     _with_codec(monkeypatch, True)
     lib = n5._native()
     p = str(tmp_path / 's.n5')
-    data = np.arange(8 * 16 * 16 * 12, dtype=np.uint64).reshape(8, 16, 16 * 12)
+    nb = 24
+    data = np.arange(8 * 16 * 16 * nb, dtype=np.uint64).reshape(8, 16, 16 * nb)
     with n5.File(p) as f:
         ds = f.create_dataset('d', shape=data.shape, chunks=(8, 16, 16), dtype='uint64', compression='gzip')
         ds[:] = data
@@ -432,31 +436,32 @@ def test_native_readahead_follows_the_job_stride(tmp_path, monkeypatch):
             lib.ctg_io_cache_stats(out.ctypes.data_as(ctypes.c_void_p))
             return out
 
-        def settle(before):
-            for _ in range(200):   # the readahead pool works in the background
+        def settle(before, n):
+            for _ in range(300):   # the readahead pool works in the background
                 s = stats()
-                if s[2] > before[2]:
-                    return s
+                if s[2] - before[2] >= n:
+                    break
                 time.sleep(0.01)
+            time.sleep(0.05)
             return stats()
 
         def read(i):
             np.testing.assert_array_equal(ds[:, :, 16 * i:16 * i + 16], data[:, :, 16 * i:16 * i + 16])
 
         s0 = stats()
-        read(0)                  # no history: the C-order successor (block 1) is queued
-        s1 = settle(s0)
-        assert s1[1] - s0[1] == 1 and s1[2] - s0[2] == 1
-        read(3)                  # stride 3: block 6 is queued
-        s2 = settle(s1)
-        assert s2[1] - s1[1] == 1 and s2[2] - s1[2] == 1
-        read(6)                  # served by the readahead; block 9 queued next
-        s3 = settle(s2)
-        assert s3[0] - s2[0] == 1 and s3[1] == s2[1] and s3[2] - s2[2] == 1
-        read(9)                  # hit again; the next guess (12) leaves the grid: nothing queued
+        read(0)                  # no history: the C-order successors 1..8 are queued
+        s1 = settle(s0, 8)
+        assert s1[1] - s0[1] == 1 and s1[2] - s0[2] == 8
+        read(3)                  # a hit; stride 3: 6 (known), 9, 12, 15, 18, 21 queued (24 leaves the grid)
+        s2 = settle(s1, 5)
+        assert s2[0] - s1[0] == 1 and s2[1] == s1[1] and s2[2] - s1[2] == 5
+        for i in (6, 9, 12, 15, 18, 21):   # every one served by the readahead, nothing more queued
+            read(i)
         time.sleep(0.1)
-        s4 = stats()
-        assert s4[0] - s3[0] == 1 and s4[1] == s3[1] and s4[2] == s3[2]
+        s3 = stats()
+        assert s3[0] - s2[0] == 6 and s3[1] == s2[1] and s3[2] == s2[2]
+        read(10)                 # never queued along the stride: decoded by the caller
+        assert stats()[1] - s3[1] == 1
     lib.ctg_io_cache_clear()
 
 
