@@ -42,7 +42,8 @@ hipError_t launch_max_pairs(int64_t n, const uint64_t* uv, unsigned long long* o
 hipError_t launch_reduce(int64_t E, const uint32_t* dE, const uint64_t* uniq, const uint32_t* runs,
                          const uint32_t* offs, const uint32_t* perm32, const uint64_t* perm64, int ib,
                          const RecordBuf& R, int wide, int stats, int nb, uint64_t umask, int need_adj,
-                         int ignore_label, double scale, double offset, const ReduceOut& O, hipStream_t s);
+                         int ignore_label, double scale, double offset, const ReduceOut& O, hipStream_t s, uint32_t* heavy = nullptr,
+                         uint32_t* n_heavy = nullptr);
 hipError_t launch_unique_blocks(const void* L, int label_bits, const BlockGeom* blocks, const uint32_t* tile_prefix,
                                 int n_blocks, int64_t n_tiles, uint64_t* out, unsigned long long* count, int64_t cap,
                                 hipStream_t s);
@@ -464,9 +465,13 @@ static hipError_t reduce_records(Workspace& w, const ReduceJob& J, hipStream_t s
 #else
     O.ablate = 0;
 #endif
+    // features-only narrow reduce: edges past 2^16 samples are listed for the
+    // wide-histogram kernel (w.small[40]: their count)
+    uint32_t* heavy = (!J.wide && J.stats && !O.wstats) ? (uint32_t*)dalloc(n * 4) : nullptr;
     e = launch_reduce(n, dE_all, w.uniq, w.runs, w.offs, packed ? nullptr : w.idx_out, packed ? w.sk_out : nullptr,
                       packed ? ib : 0, J.R, J.wide, J.stats, nb, J.umask, J.need_adj, J.ignore_label, J.scale, J.offset,
-                      O, s);
+                      O, s, heavy, heavy ? w.small + 40 : nullptr);
+    dfree(heavy);   // stream-ordered reuse
     if (e != hipSuccess) return e;
     if (may_drop) {
         ROCPRIM_CALL(w, rocprim::exclusive_scan(t, tbytes, w.keep, w.pos, 0u, (size_t)n, rocprim::plus<uint32_t>(), s));

@@ -87,6 +87,20 @@ __device__ __forceinline__ void load_record(const RecordBuf& R, uint32_t i, uint
     }
 }
 
+// an edge's records: sorted positions [b, b + n); the next slot index is loaded
+// while this record's body is in flight (one global latency per record, not two)
+template <bool WIDE>
+__device__ __forceinline__ void accumulate_run(const Perm& perm, const RecordBuf& R, uint32_t b, uint32_t n,
+                                               uint32_t (&h)[NSLOTS], uint32_t& cnt, uint32_t& flags, uint32_t& mn,
+                                               uint32_t& mx, Moments& mo) {
+    uint32_t i = n ? perm(b) : 0u;
+    for (uint32_t r = b; r < b + n; ++r) {
+        const uint32_t nxt = r + 1 < b + n ? perm(r + 1) : 0u;
+        load_record<WIDE>(R, i, h, cnt, flags, mn, mx, mo);
+        i = nxt;
+    }
+}
+
 // per-edge epilogue of the reduce: keep flag, mergeable stats row; the feature
 // row is returned in registers (k_reduce_edges stages it for coalesced stores)
 __device__ __forceinline__ void reduce_epilogue(int64_t e, uint64_t u, uint32_t (&h)[NSLOTS], uint32_t cnt,
@@ -192,14 +206,7 @@ __global__ __launch_bounds__(256) void k_reduce_edges(int64_t E, const uint32_t*
             } else
 #endif
             {
-                // the next slot index is loaded while this record's body is in
-                // flight: one global latency per record instead of two
-                uint32_t i = n ? perm(b) : 0u;
-                for (uint32_t r = b; r < b + n; ++r) {
-                    const uint32_t nxt = r + 1 < b + n ? perm(r + 1) : 0u;
-                    load_record<WIDE>(R, i, h, cnt, flags, mn, mx, mo);
-                    i = nxt;
-                }
+                accumulate_run<WIDE>(perm, R, b, n, h, cnt, flags, mn, mx, mo);
             }
             reduce_epilogue(e, u, h, cnt, flags, mn, mx, mo, umask, need_adj, ignore_label, scale, offset, O, row);
         }
@@ -214,6 +221,110 @@ __global__ __launch_bounds__(256) void k_reduce_edges(int64_t E, const uint32_t*
         }
 #endif
         store_rows_staged(stage[threadIdx.x >> 6], row, reinterpret_cast<double2*>(O.feats), e0, En);
+    }
+}
+
+// one narrow record into a packed histogram: its 21 u16-pair words are added
+// as they are (no slot can wrap while the edge's count stays below 2^16)
+__device__ __forceinline__ void add_narrow_packed(const uint4* p, uint32_t (&hp)[HWORDS], uint32_t& cnt,
+                                                  uint32_t& flags, uint32_t& mn, uint32_t& mx, Moments& mo) {
+    const double2 sw = *reinterpret_cast<const double2*>(p);
+    uint32_t w[NREC_WORDS];
+#pragma unroll
+    for (int j = 0; j < NREC_WORDS / 4; ++j) {
+        const uint4 v = p[1 + j];
+        w[4 * j] = v.x; w[4 * j + 1] = v.y; w[4 * j + 2] = v.z; w[4 * j + 3] = v.w;
+    }
+    const uint32_t piv = p[7].x;
+#pragma unroll
+    for (int j = 0; j < HWORDS; ++j) hp[j] += w[j];
+    const uint32_t n = w[21] & ~ADJ_FLAG;
+    cnt += n;
+    flags |= w[21] & ADJ_FLAG;
+    mn = min(mn, w[22]);
+    mx = max(mx, w[23]);
+    mo.add(n, sw.x, sw.y, piv);
+}
+
+// Features-only reduce of narrow records (no mergeable statistics rows): the
+// histogram stays packed, 21 u16-pair words instead of 42 slots (configs[4]
+// reduce 5.35 -> 5.17 ms; squeezed to 96 VGPRs for a fifth wave per SIMD it
+// spills and takes 7.05 ms).  An edge with more than 65535 samples (a slot
+// could have wrapped) is listed in `heavy` and redone by k_reduce_heavy with
+// the wide histogram; its row here is not used.
+#ifndef CTG_REDUCE_MINB
+#define CTG_REDUCE_MINB 4   // workgroups of 4 waves per CU (5 fits 96 VGPRs only by spilling: slower)
+#endif
+#ifndef CTG_REDUCE_PACKED
+#define CTG_REDUCE_PACKED 1   // 0: features-only calls take k_reduce_edges too (variant builds)
+#endif
+__global__ __launch_bounds__(256, CTG_REDUCE_MINB) void k_reduce_packed(int64_t E, const uint32_t* __restrict__ dE,
+                                                          const uint64_t* __restrict__ uniq,
+                                                          const uint32_t* __restrict__ runs,
+                                                          const uint32_t* __restrict__ offs, Perm perm, RecordBuf R,
+                                                          int nb, uint64_t umask, int need_adj, int ignore_label,
+                                                          double scale, double offset, ReduceOut O,
+                                                          uint32_t* __restrict__ heavy, uint32_t* __restrict__ n_heavy) {
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e == 0 && O.count_out) *O.count_out = *dE;
+    const int64_t En = min(E, (int64_t)*dE);
+    __shared__ double2 stage[256 / 64][64 * (N_FEATURES / 2)];
+    const int64_t e0 = e - (threadIdx.x & 63);
+    if (e0 >= En) return;
+    double2 row[5];
+    if (e < En) {
+        const uint64_t sk = uniq[e];
+        const uint64_t u = sk >> nb, v = sk & ((1ull << nb) - 1ull);
+        O.edges[2 * e] = u;
+        O.edges[2 * e + 1] = v;
+        uint32_t hp[HWORDS];
+#pragma unroll
+        for (int j = 0; j < HWORDS; ++j) hp[j] = 0;
+        uint32_t cnt = 0, flags = 0, mn = ORD_POS_INF, mx = ORD_NEG_INF;
+        Moments mo;
+        const uint32_t b = offs[e], n = runs[e];
+        uint32_t i = n ? perm(b) : 0u;
+        for (uint32_t r = b; r < b + n; ++r) {
+            const uint32_t nxt = r + 1 < b + n ? perm(r + 1) : 0u;
+            add_narrow_packed(reinterpret_cast<const uint4*>(R.hist + (size_t)i * NREC_STRIDE), hp, cnt, flags, mn,
+                              mx, mo);
+            i = nxt;
+        }
+        if (cnt > 0xFFFFu) {
+            heavy[atomicAdd(n_heavy, 1u)] = (uint32_t)e;
+        } else {
+            if (need_adj == 0) flags |= ADJ_FLAG;
+            if (O.keep)
+                O.keep[e] = ((need_adj == 2 || (flags & ADJ_FLAG)) && !(ignore_label && (u & umask) == 0)) ? 1u : 0u;
+            finalize_vals(PackedHist{hp}, cnt, mn, mx, mo, scale, offset, row);
+        }
+    }
+    store_rows_staged(stage[threadIdx.x >> 6], row, reinterpret_cast<double2*>(O.feats), e0, En);
+}
+
+// the listed edges of k_reduce_packed, with the wide histogram (grid-stride)
+__global__ __launch_bounds__(256) void k_reduce_heavy(const uint32_t* __restrict__ heavy,
+                                                      const uint32_t* __restrict__ n_heavy,
+                                                      const uint32_t* __restrict__ runs,
+                                                      const uint32_t* __restrict__ offs, Perm perm, RecordBuf R,
+                                                      const uint64_t* __restrict__ uniq, int nb, uint64_t umask,
+                                                      int need_adj, int ignore_label, double scale, double offset,
+                                                      ReduceOut O) {
+    const uint32_t nh = *n_heavy;
+    for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < nh; k += gridDim.x * blockDim.x) {
+        const int64_t e = heavy[k];
+        uint32_t h[NSLOTS];
+#pragma unroll
+        for (int j = 0; j < NSLOTS; ++j) h[j] = 0;
+        uint32_t cnt = 0, flags = 0, mn = ORD_POS_INF, mx = ORD_NEG_INF;
+        Moments mo;
+        accumulate_run<false>(perm, R, offs[e], runs[e], h, cnt, flags, mn, mx, mo);
+        double2 row[5];
+        reduce_epilogue(e, uniq[e] >> nb, h, cnt, flags, mn, mx, mo, umask, need_adj, ignore_label, scale, offset, O,
+                        row);
+        double2* o = reinterpret_cast<double2*>(O.feats + (size_t)e * N_FEATURES);
+#pragma unroll
+        for (int j = 0; j < N_FEATURES / 2; ++j) o[j] = row[j];
     }
 }
 
@@ -579,10 +690,21 @@ hipError_t launch_max_pairs(int64_t n, const uint64_t* uv, unsigned long long* o
 hipError_t launch_reduce(int64_t E, const uint32_t* dE, const uint64_t* uniq, const uint32_t* runs,
                          const uint32_t* offs, const uint32_t* perm32, const uint64_t* perm64, int ib,
                          const RecordBuf& R, int wide, int stats, int nb, uint64_t umask, int need_adj,
-                         int ignore_label, double scale, double offset, const ReduceOut& O, hipStream_t s) {
+                         int ignore_label, double scale, double offset, const ReduceOut& O, hipStream_t s,
+                         uint32_t* heavy, uint32_t* n_heavy) {
     if (E == 0) return hipSuccess;
     const Perm perm{perm32, perm64, ib};
     dim3 g((unsigned)((E + 255) / 256)), b(256);
+    if (CTG_REDUCE_PACKED && !wide && stats && O.feats && !O.wstats && !O.ablate && heavy && n_heavy) {
+        // features only: the packed-histogram kernel, then its heavy edges
+        hipError_t e = hipMemsetAsync(n_heavy, 0, 4, s);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(k_reduce_packed, g, b, 0, s, E, dE, uniq, runs, offs, perm, R, nb, umask, need_adj,
+                           ignore_label, scale, offset, O, heavy, n_heavy);
+        hipLaunchKernelGGL(k_reduce_heavy, dim3((unsigned)std::min<int64_t>((E + 255) / 256, 1024)), b, 0, s, heavy,
+                           n_heavy, runs, offs, perm, R, uniq, nb, umask, need_adj, ignore_label, scale, offset, O);
+        return hipGetLastError();
+    }
     if (wide) {
         if (stats) hipLaunchKernelGGL((k_reduce_edges<true, true>), g, b, 0, s, E, dE, uniq, runs, offs, perm, R, nb, umask, need_adj, ignore_label, scale, offset, O);
         else hipLaunchKernelGGL((k_reduce_edges<true, false>), g, b, 0, s, E, dE, uniq, runs, offs, perm, R, nb, umask, need_adj, ignore_label, scale, offset, O);

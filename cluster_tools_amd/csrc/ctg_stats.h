@@ -218,7 +218,15 @@ __device__ __forceinline__ void wide_row(const uint32_t (&h)[NSLOTS], uint32_t c
 // The 10 feature columns of one edge from its combined statistics (count, the
 // 42-slot histogram, ordered min / max, shifted sums about mo.p0) as five
 // column pairs in registers; an edge without samples gets a zero row.
-__device__ __forceinline__ void finalize_vals(const uint32_t (&h)[NSLOTS], uint32_t cnt, uint32_t mn, uint32_t mx,
+// the 42 u16 slots of a histogram kept as 21 u16-pair words (the narrow
+// record's own packing), read slot by slot (constant slots after unrolling)
+struct PackedHist {
+    const uint32_t* w;
+    __device__ __forceinline__ uint32_t operator[](int k) const { return (w[k >> 1] >> ((k & 1) * 16)) & 0xFFFFu; }
+};
+
+template <typename HL>
+__device__ __forceinline__ void finalize_vals(const HL& h, uint32_t cnt, uint32_t mn, uint32_t mx,
                                               const Moments& mo, double scale, double offset, double2 (&r)[5],
                                               bool quantiles = true) {
     if (cnt == 0) {

@@ -711,6 +711,27 @@ def test_narrow_tile_matches_wide_tile(gpu, monkeypatch, shape, cell, quant):
     check_features(out['features'], f_o)
 
 
+def test_heavy_and_light_edges(gpu):
+    """The features-only reduce keeps each edge's histogram as 21 u16-pair
+    words while its count stays below 2^16; an edge past that (here the
+    131072-sample face between two 256 x 256 slabs) is listed and redone with
+    the wide histogram.  Heavy and light edges together, against the oracle:
+    every column, quantiles included."""
+    small, _ = S.generate((4, 256, 256), cell=6, seed=31)
+    lab = np.empty((12, 256, 256), np.uint64)
+    lab[:4] = small + np.uint64(10)
+    lab[4:8] = 1
+    lab[8:] = 2
+    rng = np.random.default_rng(31)
+    bnd = rng.random(lab.shape, dtype=np.float32)
+    out = rag.rag_features(lab, bnd)
+    e_ref, f_ref = O.boundary_features(lab, bnd)
+    np.testing.assert_array_equal(out['edges'], e_ref)
+    check_features(out['features'], f_ref)
+    k = int(np.flatnonzero((e_ref[:, 0] == 1) & (e_ref[:, 1] == 2))[0])
+    assert out['features'][k, 9] == 2 * 256 * 256 and out['features'][:, 9].max() == 2 * 256 * 256
+
+
 def test_single_edge_many_records(gpu, monkeypatch):
     """One edge with a record from every tile: two planes of two labels over
     4096 x 4096 (8192 (1, 2) records, all in one bucket and one in-bucket
