@@ -333,7 +333,9 @@ constexpr int GS_PASS_THREADS = 1024;         // bucket passes
 constexpr int GS_CHUNK = GS_PASS_THREADS * GS_IPT; // records per workgroup of the bucket passes
 constexpr int GS_BB_MAX = 16;                 // 64 K buckets
 constexpr int GS_M = 1 << GS_BB_MAX;
-constexpr uint32_t GS_HALF = 32768;           // LDS bucket counters per pass of the bucket kernels (128 KB)
+constexpr uint32_t GS_HALF = 8192;            // LDS bucket counters per window pass of the bucket kernels (32 KB:
+                                              // two 1024-thread workgroups per CU; a workgroup's bucket range
+                                              // is usually far narrower, a wider one takes several passes)
 constexpr int GS_GB = 11;                     // group bits of the in-bucket counting sort
 constexpr int GS_NG = 1 << GS_GB;
 constexpr uint64_t GS_HEAD = 1ull << 63;      // sorted key of a run head (keys use at most 63 bits)
@@ -418,7 +420,7 @@ __global__ __launch_bounds__(GS_PASS_THREADS) void k_gs_hist(GsParams P, uint32_
     __shared__ uint32_t red[2];
     uint32_t lo, hi;
     gs_bucket_range(bk, red, lo, hi);
-    // [lo, hi] in windows of at most GS_HALF counters (128 KB)
+    // [lo, hi] in windows of at most GS_HALF counters
     for (uint32_t h0 = lo; h0 <= hi && lo <= hi; h0 += GS_HALF) {
         const uint32_t hn = min(GS_HALF, hi + 1 - h0);
         for (uint32_t i = threadIdx.x; i < hn; i += GS_PASS_THREADS) h[i] = 0;
